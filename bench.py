@@ -1,0 +1,243 @@
+#!/usr/bin/env python3
+"""Throughput of the PSO inverse-kinematics hot path on MI355X.
+
+One step = one batch of independent IK solves (one swarm per target) on every
+rank: BASELINE config 3 per GPU -- the reference's 7-joint (21-DOF) scene,
+4096 perturbed targets, 1024 particles per swarm, 500 PSO iterations -- then
+one all-gather of the per-swarm results (RCCL over xGMI) and a copy of the
+gathered results to the host.  Inputs (targets) are resident in HBM before the
+timed region.  Weak scaling: per-GPU work is fixed, N GPUs solve N x 4096
+targets (N = 8 is 32768 targets; `--swarms-per-gpu 8192` gives config 4's
+65536).  Generator seeds are global (swarm b, particle i: curand_init(b*1024+i)).
+
+Prints ONE JSON line on rank 0 (see DESIGN.md for every field).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT / "inverse-kinematics-pso-research_amd"))
+
+# MI355X constants (MI355X_MICROARCH.md "Chip-level parameters")
+HBM_PEAK_GBS = 8000.0
+CUS, SIMDS, LANES_PER_CLK, CLOCK_GHZ = 256, 4, 32, 2.4
+VALU_PEAK_TINSTR = CUS * SIMDS * LANES_PER_CLK * CLOCK_GHZ / 1e3  # lane-instructions/s, 78.6 T
+# algorithmic bytes per particle-update = 20*D + 8 (x, v, pbest read; x, v written; pbest fitness r/w)
+ALG_BYTES_PER_UPDATE_D21 = 20 * 21 + 8
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--swarms-per-gpu", type=int, default=4096)
+    ap.add_argument("--particles", type=int, default=1024)
+    ap.add_argument("--iterations", type=int, default=500)
+    ap.add_argument("--arith", choices=["fast", "reference"], default="fast")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU baseline sample (0 = skip)")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    return ap.parse_args()
+
+
+def valu_per_update():
+    """VALU lane-instructions per particle-update of the resident kernel, from
+    the committed rocprofv3 SQ_INSTS_VALU measurement (profiles/), else None."""
+    f = ROOT / "profiles" / "valu_per_update.json"
+    if f.exists():
+        try:
+            return json.loads(f.read_text())
+        except Exception:
+            return None
+    return None
+
+
+def cpu_baseline(wl, seconds: float, threads: int):
+    """The CPU oracle (reference algorithm restated in C, reference 4x4 FK
+    order) on a bounded sample of the same workload: batches of `threads`
+    swarms (1024 particles, 500 iterations, the same targets and seeds) until
+    `seconds` of wall time have elapsed."""
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import oracle
+
+    oracle.load()
+    P, I = wl.particles, wl.iterations
+    done, t0, first = 0, time.perf_counter(), 0
+    while True:
+        B = threads
+        tg = wl.targets(first, B)
+        rng = oracle.init_generators(B * P, first * P)
+        oracle.solve_batch(wl.chain, tg, None, P, I, rng, threads=threads)
+        done += B
+        first += B
+        el = time.perf_counter() - t0
+        if el >= seconds or done >= 64 * threads:
+            break
+    ups = done * P * I / el
+    return {"value": ups, "unit": "particle-updates/s", "cores": threads, "kind": "port",
+            "solves_per_s": done / el,
+            "sample": f"{done} swarms x {P} particles x {I} iterations of config 3 (same targets/seeds), "
+                      f"OpenMP over swarms, {el:.1f} s"}
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    import ikpso
+    from ikpso import dist as idist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", torch.cuda.current_device())
+
+    wl = ikpso.workload(3)
+    P, I = args.particles, args.iterations
+    Bl = args.swarms_per_gpu
+    total = Bl * world
+    first = rank * Bl
+    targets = torch.from_numpy(wl.targets(first, Bl)).to(dev)
+    solver = ikpso.BatchSolver(wl.chain, P, pso=ikpso.PSOConfig(0.5, 0.5, 1.25, I), arith=args.arith)
+    solver.seed(Bl, seed_base=0, first_swarm=first)
+    D = solver.dof
+    out = (torch.empty((Bl, D), device=dev), torch.empty((Bl,), device=dev), torch.empty((Bl,), device=dev))
+    host = torch.empty((total, D + 2), dtype=torch.float32, pin_memory=True)
+
+    def step(evs=None):
+        if evs is not None:
+            evs[0].record()
+        solver.solve(targets, iterations=I, out=out)
+        if evs is not None:
+            evs[1].record()
+        rows = idist.pack_results(*out)
+        if world > 1:
+            rows = idist.gather_rows(rows, total, world)
+        host.copy_(rows, non_blocking=True)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(evs[k])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed, kern_ms = float(t[0]), float(t[1])
+
+    ups_step = total * P * I
+    value = ups_step * args.steps / elapsed
+    # results sanity: finite, and the gathered rows are what each rank solved
+    res = host.numpy()
+    finite = bool(np.isfinite(res).all())
+    mean_fit = float(res[:, D].mean())
+    mean_res = float(res[:, D + 1].mean())
+
+    single_ms = None
+    if rank == 0:
+        s2 = ikpso.BatchSolver(wl.chain, P, pso=ikpso.PSOConfig(0.5, 0.5, 1.25, I), arith=args.arith)
+        s2.seed(1)
+        tg1 = targets[:1].contiguous()
+        s2.solve(tg1, iterations=I)
+        torch.cuda.synchronize()
+        ts = []
+        for _ in range(5):
+            a = time.perf_counter()
+            r = s2.solve(tg1, iterations=I)
+            r[0].cpu()
+            ts.append(time.perf_counter() - a)
+        single_ms = 1e3 * float(np.median(ts))
+        s2.close()
+
+    if rank == 0:
+        ups_launch = Bl * P * I
+        kern_s = kern_ms / 1e3
+        alg_gbs = ups_launch * ALG_BYTES_PER_UPDATE_D21 / kern_s / 1e9
+        vpu = valu_per_update()
+        valu = None
+        if vpu:
+            ach = ups_launch * vpu["valu_lane_instr_per_update"] / kern_s / 1e12
+            valu = {"achieved": round(ach, 2), "peak": round(VALU_PEAK_TINSTR, 1), "unit": "Tlane-instr/s",
+                    "frac": round(ach / VALU_PEAK_TINSTR, 4),
+                    "instr_per_update": vpu["valu_lane_instr_per_update"], "source": vpu.get("source")}
+        roofline = {
+            "bound": "valu" if valu else "hbm",
+            "achieved": valu["achieved"] if valu else round(alg_gbs, 1),
+            "peak": valu["peak"] if valu else HBM_PEAK_GBS,
+            "unit": valu["unit"] if valu else "GB/s",
+            "frac": valu["frac"] if valu else round(alg_gbs / HBM_PEAK_GBS, 4),
+            "traffic": vpu.get("hbm_bytes_per_launch") if vpu else None,
+            "kernel": "k_swarm_resident<TopoRef7,FAST> (one launch = one batch)",
+            "kernel_ms": round(kern_ms, 3),
+            "hbm_algorithmic": {
+                "achieved": round(alg_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(alg_gbs / HBM_PEAK_GBS, 4),
+                "bytes_per_update": ALG_BYTES_PER_UPDATE_D21,
+                "note": "SURVEY §8(d) north-star formulation (x/v/pbest streamed through HBM every iteration); "
+                        "this kernel keeps them on chip, so the figure can exceed 1 and the binding roof is VALU",
+            },
+        }
+        cpu = None
+        if world == 1 and args.cpu_seconds > 0:
+            cpu = cpu_baseline(wl, args.cpu_seconds, args.cpu_threads)
+        line = {
+            "metric": "PSO particle-updates/sec + IK solves/sec, 7-DOF 1024-particle swarm",
+            "value": value,
+            "unit": "particle-updates/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": 1e3 * elapsed / args.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (seeded targets: reset targets + U[-0.25,0.25]^3 per effector)",
+            "config": {
+                "workload": "config3: 7-joint (21-DOF) reference scene, 1024-particle swarms, 500 PSO iterations, "
+                            f"{Bl} targets per GPU ({total} total)",
+                "swarms_per_gpu": Bl, "total_swarms": total, "particles": P, "iterations": I, "dof": D,
+                "parallelism": f"dp{world} (swarm shards) + RCCL all-gather of results" if world > 1
+                else "1 GPU",
+                "arith": args.arith,
+            },
+            "solves_per_s": total * args.steps / elapsed,
+            "single_solve_ms": single_ms,
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+            "check": {"finite": finite, "mean_fitness": mean_fit, "mean_residual": mean_res},
+        }
+        if valu:
+            line["roofline"]["valu"] = valu
+        print(json.dumps(line), flush=True)
+    solver.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

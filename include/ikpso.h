@@ -1,0 +1,194 @@
+/*
+ * ikpso.h -- C ABI of the MI355X-native PSO inverse-kinematics solver.
+ *
+ * This is the drop-in boundary for the reference's solver hot path
+ * (MadDevX/Inverse-Kinematics-PSO-Research, src/ = InverseKinematicsResearch/
+ * InverseKinematicsResearch/).  Plain C types, plain pointers and sizes; no
+ * torch or C++ types.  Every entry point returns an ikpso_status (0 = success,
+ * mirroring cudaSuccess/hipSuccess: the reference's caller aborts its frame
+ * loop on any non-zero value, src/Main.cpp:225-226).
+ *
+ * Memory: "device" pointers are HIP device allocations (hipMalloc) or managed
+ * allocations (hipMallocManaged); "any" pointers may be host, managed or device
+ * memory (copied with hipMemcpyDefault).  Stream: a hipStream_t passed as
+ * void*; NULL = the legacy default stream.  Calls are stream-ordered; the
+ * reference-compatible entry points additionally synchronise before returning,
+ * as the reference does (src/kernel.cu:317-322).
+ */
+#ifndef IKPSO_H
+#define IKPSO_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define IKPSO_ABI_VERSION 1
+
+typedef int ikpso_status;
+enum {
+    IKPSO_OK = 0,
+    IKPSO_ERR_INVALID_ARG = 1,   /* bad size, null pointer, bad node table */
+    IKPSO_ERR_UNSUPPORTED = 2,   /* e.g. colliderCount > 0 (GJK term not built yet) */
+    IKPSO_ERR_HIP = 3,           /* a HIP runtime call failed; see ikpso_last_hip_error() */
+    IKPSO_ERR_NO_MEMORY = 4
+};
+
+/* Node types, same values as the reference's NodeType (src/Particle.h:10-15). */
+enum { IKPSO_NODE_ORIGIN = 0, IKPSO_NODE_EFFECTOR = 1, IKPSO_NODE = 2 };
+
+/* One node of the kinematic tree; byte-identical to the reference's NodeCUDA
+ * (src/Particle.h:24-39, 88 bytes).  Node 0 is the origin; nodes 1..J are
+ * 3-axis Euler-XYZ joints followed by a link of `length` along local +X
+ * (src/kernel.cu:52-56); parent_index < own index (DFS order, src/Node.h:232-267). */
+typedef struct ikpso_node {
+    int32_t node_type;
+    int32_t parent_index;
+    float effector_weight;
+    float position[3];        /* origin only */
+    float rotation[3];        /* current pose = warm start + angle-term reference */
+    float max_rotation[3];    /* clamp bounds, per Euler axis */
+    float min_rotation[3];
+    float length;
+    float target_position[3]; /* effectors only */
+    float target_rotation[3]; /* unused by the fitness (as in the reference) */
+} ikpso_node;
+
+/* XORWOW generator state with cuRAND's curandStateXORWOW layout (48 bytes),
+ * so N * sizeof(curandState_t) allocations stay valid (src/Main.cpp:137). */
+typedef struct ikpso_rng_state {
+    uint32_t d;
+    uint32_t v[5];
+    int32_t boxmuller_flag;
+    int32_t boxmuller_flag_double;
+    float boxmuller_extra;
+    uint32_t pad_;
+    double boxmuller_extra_double;
+} ikpso_rng_state;
+
+/* PSOConfig (src/Particle.h:70-85): passed by value like the reference. */
+typedef struct ikpso_pso_config {
+    float inertia;
+    float local;
+    float global;
+    int32_t iterations;
+} ikpso_pso_config;
+
+/* FitnessConfig (src/Particle.h:55-68). */
+typedef struct ikpso_fitness_config {
+    float angle_weight;
+    float distance_weight;
+    float error_threshold; /* never read, as in the reference */
+} ikpso_fitness_config;
+
+/* obj_t (src/BoxCollider.h:4-10): box half-extents, centre, orientation quaternion. */
+typedef struct ikpso_collider {
+    float x, y, z;
+    float pos[3];
+    float pad_[2];
+    float quat[4]; /* float4, 16-byte aligned in the reference */
+} ikpso_collider;
+
+/* Arithmetic mode of the device kernels. */
+enum {
+    IKPSO_ARITH_FAST = 0,      /* closed-form 3x3 FK, FMA contraction (default) */
+    IKPSO_ARITH_REFERENCE = 1  /* the reference's 4x4 operation order, no FMA contraction */
+};
+
+/* ---------------------------------------------------------------------------
+ * Reference-compatible entry points (single swarm).
+ * ------------------------------------------------------------------------- */
+
+/* Replaces initGenerators (src/utility_kernels.cuh:33-47, declared at
+ * src/Main.cpp:28): randoms[i] = curand_init(i, 0, 0).  randoms: device. */
+ikpso_status ikpso_init_generators(ikpso_rng_state* randoms, int size, void* stream);
+
+/* Generalised seeding: randoms[i] = curand_init(seed_base + i, 0, 0). */
+ikpso_status ikpso_init_generators_seeded(ikpso_rng_state* randoms, int64_t count, uint64_t seed_base,
+                                          void* stream);
+
+/* Replaces calculatePSO (src/kernel.cu:279-327, declared at src/Main.cpp:29).
+ *   particles [3][D][size] floats, device: SoA position / velocity / local best
+ *             (src/kernel.cu:17-29); overwritten with the final swarm state.
+ *   positions [4*J] floats, any: host-computed arm positions, read only when
+ *             fit.distance_weight != 0, at slot (k-1)*4 for node k (src/kernel.cu:94-98).
+ *   bests     [size] floats, device: final local-best fitness per particle.
+ *   randoms   [size] states, device: consumed and advanced (persist across calls).
+ *   chain     [node_count] nodes, any.  D = 3*(node_count-1).
+ *   result    [D] floats, any: global-best joint angles (Coordinates).
+ *   colliders/collider_count: collider_count must be 0 (IKPSO_ERR_UNSUPPORTED otherwise).
+ * Synchronises `stream` before returning. */
+ikpso_status ikpso_calculate_pso(float* particles, const float* positions, float* bests,
+                                 ikpso_rng_state* randoms, int size, const ikpso_node* chain, int node_count,
+                                 ikpso_pso_config pso, ikpso_fitness_config fit, float* result,
+                                 const ikpso_collider* colliders, int collider_count, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Batched API: B independent swarms (IK targets) per call, one launch.
+ * ------------------------------------------------------------------------- */
+
+typedef struct ikpso_solver ikpso_solver;
+
+typedef struct ikpso_solver_desc {
+    const ikpso_node* chain;  /* any; node table shared by every swarm */
+    int32_t node_count;       /* J + 1 */
+    int32_t particles;        /* P per swarm */
+    ikpso_pso_config pso;
+    ikpso_fitness_config fit;
+    int32_t arith;            /* IKPSO_ARITH_* */
+    int32_t reserved0;
+    const float* positions;   /* any, [4*J] or NULL (distance term, as calculatePSO) */
+    /* Optional soft joint-limit penalty (a new term; the reference only clamps):
+     * fitness += limit_weight * sum_d max(0, x_d - soft_hi[d], soft_lo[d] - x_d)^2 */
+    float limit_weight;
+    float reserved1;
+    const float* soft_lo;     /* any, [D] or NULL */
+    const float* soft_hi;     /* any, [D] or NULL */
+} ikpso_solver_desc;
+
+ikpso_status ikpso_solver_create(const ikpso_solver_desc* desc, ikpso_solver** out);
+ikpso_status ikpso_solver_destroy(ikpso_solver* solver);
+
+/* Allocate (or re-seed) the solver-owned generator states for `capacity`
+ * swarms: state of local swarm b, particle i = curand_init(seed_base +
+ * (first_swarm + b) * P + i, 0, 0).  first_swarm is the global index of local
+ * swarm 0, so a batch sharded over ranks draws the same streams as one rank.
+ * States persist across solve calls (like the reference's randoms buffer). */
+ikpso_status ikpso_solver_seed(ikpso_solver* solver, int64_t capacity, uint64_t seed_base, int64_t first_swarm,
+                               void* stream);
+
+/* Solve `num_swarms` (<= capacity) swarms for `iterations` PSO iterations.
+ *   targets    device, [B][E][3]: effector targets, effectors in node order.
+ *   start_pose device, [B][D] or NULL (NULL: chain rotations).
+ *   out_angles device [B][D]; out_fitness device [B]; out_residual device [B] or NULL
+ *   (residual = sum over effectors of |p_e - t_e|, as checkDistance).
+ * Stream-ordered; does not synchronise. */
+ikpso_status ikpso_solve_batch(ikpso_solver* solver, const float* targets, const float* start_pose,
+                               int64_t num_swarms, int32_t iterations, float* out_angles, float* out_fitness,
+                               float* out_residual, void* stream);
+
+/* Evaluate the device FK + fitness for n angle vectors (no PSO):
+ *   angles device [n][D]; targets device [n][E][3] or NULL (chain targets);
+ *   rest device [n][D] or NULL (chain rotations); out_fitness device [n] or NULL;
+ *   out_positions device [n][J][3] or NULL (world position of nodes 1..J). */
+ikpso_status ikpso_solver_evaluate(ikpso_solver* solver, const float* angles, const float* targets,
+                                   const float* rest, int64_t n, float* out_fitness, float* out_positions,
+                                   void* stream);
+
+/* Introspection. */
+int ikpso_solver_dof(const ikpso_solver* solver);
+int ikpso_solver_effectors(const ikpso_solver* solver);
+/* Name of the kernel variant the solver dispatches to (topology / residency). */
+const char* ikpso_solver_kernel_name(const ikpso_solver* solver);
+
+int ikpso_abi_version(void);
+const char* ikpso_status_string(ikpso_status status);
+int ikpso_last_hip_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* IKPSO_H */

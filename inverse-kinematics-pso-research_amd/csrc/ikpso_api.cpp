@@ -1,0 +1,404 @@
+// ikpso_api.cpp -- the C ABI (include/ikpso.h): validation, chain parsing,
+// solver handles, dispatch to the gfx950 kernels.
+#include <hip/hip_runtime.h>
+
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <mutex>
+#include <new>
+#include <vector>
+
+#include "ikpso.h"
+#include "ikpso_kernels.h"
+
+using namespace ikpso;
+
+static_assert(sizeof(ikpso_node) == 88, "ikpso_node must match NodeCUDA (88 bytes)");
+static_assert(sizeof(ikpso_rng_state) == 48, "ikpso_rng_state must match curandStateXORWOW (48 bytes)");
+static_assert(sizeof(ikpso_pso_config) == 16, "PSOConfig is 16 bytes");
+static_assert(sizeof(ikpso_fitness_config) == 12, "FitnessConfig is 12 bytes");
+static_assert(sizeof(ikpso_collider) == 48, "obj_t is 48 bytes");
+
+namespace {
+
+thread_local int g_last_hip_error = 0;
+
+ikpso_status hip_status(hipError_t e)
+{
+    if (e == hipSuccess) return IKPSO_OK;
+    g_last_hip_error = (int)e;
+    return e == hipErrorOutOfMemory ? IKPSO_ERR_NO_MEMORY : IKPSO_ERR_HIP;
+}
+
+#define IKPSO_HIP(call)                                  \
+    do {                                                 \
+        hipError_t e_ = (call);                          \
+        if (e_ != hipSuccess) return hip_status(e_);     \
+    } while (0)
+
+// ---- reference-order 4x4 host math for the origin transform M0 -----------
+// M0 = I * T(position) * Rx * Ry * Rz (src/kernel.cu:36-38), computed with
+// the reference's product order so the REFERENCE arithmetic mode reproduces
+// it bit for bit.
+struct M4 {
+    float c[16];
+};
+
+M4 m4_create(float f)
+{
+    M4 m;
+    for (float& x : m.c) x = 0.0f;
+    for (int i = 0; i < 4; ++i) m.c[i + 4 * i] = f;
+    return m;
+}
+
+M4 m4_mul(const M4& l, const M4& r)
+{
+#pragma clang fp contract(off)
+    M4 o = m4_create(0.0f);
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j) {
+            float s = 0.0f;
+            for (int x = 0; x < 4; ++x) s += l.c[x + j * 4] * r.c[x * 4 + i];
+            o.c[i + j * 4] = s;
+        }
+    return o;
+}
+
+M4 origin_matrix(const ikpso_node& n)
+{
+    M4 m = m4_create(1.0f);
+    M4 t = m4_create(1.0f);
+    t.c[3] = n.position[0];
+    t.c[7] = n.position[1];
+    t.c[11] = n.position[2];
+    m = m4_mul(m, t);
+    const float a = n.rotation[0], b = n.rotation[1], c = n.rotation[2];
+    M4 rx = m4_create(1.0f);
+    rx.c[5] = cosf(a);
+    rx.c[6] = -sinf(a);
+    rx.c[9] = sinf(a);
+    rx.c[10] = cosf(a);
+    m = m4_mul(m, rx);
+    M4 ry = m4_create(1.0f);
+    ry.c[0] = cosf(b);
+    ry.c[2] = sinf(b);
+    ry.c[8] = -sinf(b);
+    ry.c[10] = cosf(b);
+    m = m4_mul(m, ry);
+    M4 rz = m4_create(1.0f);
+    rz.c[0] = cosf(c);
+    rz.c[1] = -sinf(c);
+    rz.c[4] = sinf(c);
+    rz.c[5] = cosf(c);
+    return m4_mul(m, rz);
+}
+
+// Copy `bytes` from host, managed or device memory into host memory.
+ikpso_status fetch_any(void* dst, const void* src, size_t bytes)
+{
+    if (bytes == 0) return IKPSO_OK;
+    IKPSO_HIP(hipMemcpy(dst, src, bytes, hipMemcpyDefault));
+    return IKPSO_OK;
+}
+
+struct Extras {
+    const float* positions = nullptr;  // host copy, [4J]
+    float limit_weight = 0.0f;
+    const float* soft_lo = nullptr;    // host copies, [D]
+    const float* soft_hi = nullptr;
+};
+
+ikpso_status parse_chain(const std::vector<ikpso_node>& nodes, const ikpso_pso_config& pso,
+                         const ikpso_fitness_config& fit, const Extras& ex, ChainHost& ch)
+{
+    const int n = (int)nodes.size();
+    if (n < 2 || n - 1 > kMaxJoints) return IKPSO_ERR_INVALID_ARG;
+    const int J = n - 1;
+    ch = ChainHost{};
+    ch.J = J;
+    ch.parent.assign(J + 1, -1);
+    ch.eff_slot.assign(J + 1, -1);
+    ch.len.assign(J + 1, 0.0f);
+    ch.eff_w.assign(J + 1, 0.0f);
+    ch.lo.assign(3 * J, 0.0f);
+    ch.hi.assign(3 * J, 0.0f);
+    ch.rest.assign(3 * J, 0.0f);
+    ch.tgt0.assign(3 * J, 0.0f);
+    int E = 0;
+    bool ref7 = (J == 7), serial = true;
+    uint64_t eff_mask = 0;
+    static const int kRef7[8] = {-1, 0, 1, 2, 3, 4, 4, 4};
+    for (int k = 1; k <= J; ++k) {
+        const ikpso_node& nd = nodes[k];
+        if (nd.parent_index < 0 || nd.parent_index >= k) return IKPSO_ERR_INVALID_ARG;
+        ch.parent[k] = nd.parent_index;
+        ch.len[k] = nd.length;
+        serial = serial && nd.parent_index == k - 1;
+        if (J == 7) ref7 = ref7 && nd.parent_index == kRef7[k];
+        for (int c = 0; c < 3; ++c) {
+            ch.lo[3 * (k - 1) + c] = nd.min_rotation[c];
+            ch.hi[3 * (k - 1) + c] = nd.max_rotation[c];
+            ch.rest[3 * (k - 1) + c] = nd.rotation[c];
+        }
+        if (nd.node_type == IKPSO_NODE_EFFECTOR) {
+            eff_mask |= 1ull << k;
+            ch.eff_slot[k] = E++;
+            ch.eff_w[k] = nd.effector_weight;
+            for (int c = 0; c < 3; ++c) ch.tgt0[3 * (k - 1) + c] = nd.target_position[c];
+        }
+    }
+    ch.E = E;
+    ref7 = ref7 && eff_mask == 0xE0ull;                // effectors = nodes 5, 6, 7
+    serial = serial && eff_mask == (1ull << J);        // single tip effector
+    ch.topo = ref7 ? TopoKind::Ref7 : (serial ? TopoKind::SerialTip : TopoKind::Generic);
+    const M4 m0 = origin_matrix(nodes[0]);
+    for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 4; ++c) ch.m0[4 * r + c] = m0.c[4 * r + c];
+    ch.w = pso.inertia;
+    ch.c1 = pso.local;
+    ch.c2 = pso.global;
+    // fitConfig.{angle,distance}Weight / (DEGREES_OF_FREEDOM / 3) (src/kernel.cu:150)
+    ch.aw_j = fit.angle_weight / (float)J;
+    ch.dw_j = fit.distance_weight / (float)J;
+    ch.use_posref = fit.distance_weight != 0.0f;
+    ch.lim_w = ex.limit_weight;
+    ch.use_penalty = ex.limit_weight != 0.0f && ex.soft_lo && ex.soft_hi;
+    ch.aux.assign(10 * J, 0.0f);
+    if (ch.use_posref && ex.positions)
+        for (int i = 0; i < 4 * J; ++i) ch.aux[i] = ex.positions[i];
+    if (ch.use_penalty)
+        for (int d = 0; d < 3 * J; ++d) {
+            ch.aux[4 * J + d] = ex.soft_lo[d];
+            ch.aux[7 * J + d] = ex.soft_hi[d];
+        }
+    if (!chain_supported(ch)) return IKPSO_ERR_UNSUPPORTED;
+    return IKPSO_OK;
+}
+
+// Small device scratch for the reference-compatible path (result staging).
+std::mutex g_scratch_mu;
+float* g_scratch = nullptr;
+size_t g_scratch_bytes = 0;
+
+ikpso_status scratch(size_t bytes, float** out)
+{
+    std::lock_guard<std::mutex> lk(g_scratch_mu);
+    if (g_scratch_bytes < bytes) {
+        if (g_scratch) (void)hipFree(g_scratch);
+        g_scratch = nullptr;
+        g_scratch_bytes = 0;
+        IKPSO_HIP(hipMalloc(&g_scratch, bytes));
+        g_scratch_bytes = bytes;
+    }
+    *out = g_scratch;
+    return IKPSO_OK;
+}
+
+}  // namespace
+
+struct ikpso_solver {
+    ChainHost chain;
+    int P = 0;
+    int mode = IKPSO_ARITH_FAST;
+    ikpso_rng_state* rng = nullptr;
+    int64_t capacity = 0;
+};
+
+extern "C" {
+
+int ikpso_abi_version(void) { return IKPSO_ABI_VERSION; }
+
+int ikpso_last_hip_error(void) { return g_last_hip_error; }
+
+const char* ikpso_status_string(ikpso_status s)
+{
+    switch (s) {
+    case IKPSO_OK: return "ok";
+    case IKPSO_ERR_INVALID_ARG: return "invalid argument";
+    case IKPSO_ERR_UNSUPPORTED: return "unsupported configuration";
+    case IKPSO_ERR_HIP: return "HIP runtime error";
+    case IKPSO_ERR_NO_MEMORY: return "out of device memory";
+    default: return "unknown status";
+    }
+}
+
+ikpso_status ikpso_init_generators_seeded(ikpso_rng_state* randoms, int64_t count, uint64_t seed_base, void* stream)
+{
+    if (count < 0 || (count > 0 && !randoms)) return IKPSO_ERR_INVALID_ARG;
+    IKPSO_HIP(launch_init_generators(randoms, count, seed_base, (hipStream_t)stream));
+    return IKPSO_OK;
+}
+
+// initGenerators (src/utility_kernels.cuh:33-47): launch, then synchronise.
+ikpso_status ikpso_init_generators(ikpso_rng_state* randoms, int size, void* stream)
+{
+    ikpso_status s = ikpso_init_generators_seeded(randoms, size, 0, stream);
+    if (s != IKPSO_OK) return s;
+    IKPSO_HIP(hipStreamSynchronize((hipStream_t)stream));
+    return IKPSO_OK;
+}
+
+ikpso_status ikpso_calculate_pso(float* particles, const float* positions, float* bests, ikpso_rng_state* randoms,
+                                 int size, const ikpso_node* chain, int node_count, ikpso_pso_config pso,
+                                 ikpso_fitness_config fit, float* result, const ikpso_collider* colliders,
+                                 int collider_count, void* stream)
+{
+    (void)colliders;
+    if (collider_count > 0) return IKPSO_ERR_UNSUPPORTED;  // GJK term: not built yet
+    if (size <= 0 || !particles || !bests || !randoms || !chain || !result || node_count < 2 ||
+        node_count - 1 > kMaxJoints || pso.iterations < 0)
+        return IKPSO_ERR_INVALID_ARG;
+    std::vector<ikpso_node> nodes(node_count);
+    ikpso_status st = fetch_any(nodes.data(), chain, sizeof(ikpso_node) * node_count);
+    if (st != IKPSO_OK) return st;
+    const int J = node_count - 1, D = 3 * J;
+    std::vector<float> pos;
+    Extras ex;
+    if (fit.distance_weight != 0.0f && positions) {
+        pos.resize(4 * J);
+        st = fetch_any(pos.data(), positions, sizeof(float) * 4 * J);
+        if (st != IKPSO_OK) return st;
+        ex.positions = pos.data();
+    }
+    ChainHost ch;
+    st = parse_chain(nodes, pso, fit, ex, ch);
+    if (st != IKPSO_OK) return st;
+    if (size > resident_max_threads(ch)) return IKPSO_ERR_UNSUPPORTED;  // streaming kernels: next
+
+    float* dres = nullptr;
+    st = scratch(sizeof(float) * D, &dres);
+    if (st != IKPSO_OK) return st;
+    const hipStream_t s = (hipStream_t)stream;
+    SwarmIO io{};
+    io.targets = nullptr;
+    io.start_pose = nullptr;
+    io.rng = randoms;
+    io.out_angles = dres;
+    io.out_fitness = nullptr;
+    io.out_residual = nullptr;
+    io.dump_particles = particles;
+    io.dump_bests = bests;
+    io.P = size;
+    io.iterations = pso.iterations;
+    io.num_swarms = 1;
+    // The reference-compatible entry has no mode argument; IKPSO_ARITH=reference
+    // selects the reference's operation order (parity runs).
+    const char* env = getenv("IKPSO_ARITH");
+    const int mode = (env && strcmp(env, "reference") == 0) ? IKPSO_ARITH_REFERENCE : IKPSO_ARITH_FAST;
+    IKPSO_HIP(launch_resident(ch, mode, io, s));
+    IKPSO_HIP(hipMemcpyAsync(result, dres, sizeof(float) * D, hipMemcpyDefault, s));
+    IKPSO_HIP(hipStreamSynchronize(s));
+    return IKPSO_OK;
+}
+
+ikpso_status ikpso_solver_create(const ikpso_solver_desc* desc, ikpso_solver** out)
+{
+    if (!desc || !out || !desc->chain || desc->node_count < 2 || desc->node_count - 1 > kMaxJoints ||
+        desc->particles <= 0)
+        return IKPSO_ERR_INVALID_ARG;
+    if (desc->arith != IKPSO_ARITH_FAST && desc->arith != IKPSO_ARITH_REFERENCE) return IKPSO_ERR_INVALID_ARG;
+    *out = nullptr;
+    const int J = desc->node_count - 1, D = 3 * J;
+    std::vector<ikpso_node> nodes(desc->node_count);
+    ikpso_status st = fetch_any(nodes.data(), desc->chain, sizeof(ikpso_node) * desc->node_count);
+    if (st != IKPSO_OK) return st;
+    std::vector<float> pos, slo, shi;
+    Extras ex;
+    if (desc->fit.distance_weight != 0.0f && desc->positions) {
+        pos.resize(4 * J);
+        if ((st = fetch_any(pos.data(), desc->positions, sizeof(float) * 4 * J)) != IKPSO_OK) return st;
+        ex.positions = pos.data();
+    }
+    if (desc->limit_weight != 0.0f) {
+        if (!desc->soft_lo || !desc->soft_hi) return IKPSO_ERR_INVALID_ARG;
+        slo.resize(D);
+        shi.resize(D);
+        if ((st = fetch_any(slo.data(), desc->soft_lo, sizeof(float) * D)) != IKPSO_OK) return st;
+        if ((st = fetch_any(shi.data(), desc->soft_hi, sizeof(float) * D)) != IKPSO_OK) return st;
+        ex.limit_weight = desc->limit_weight;
+        ex.soft_lo = slo.data();
+        ex.soft_hi = shi.data();
+    }
+    ikpso_solver* s = new (std::nothrow) ikpso_solver();
+    if (!s) return IKPSO_ERR_NO_MEMORY;
+    st = parse_chain(nodes, desc->pso, desc->fit, ex, s->chain);
+    if (st != IKPSO_OK) {
+        delete s;
+        return st;
+    }
+    s->P = desc->particles;
+    s->mode = desc->arith;
+    if (s->P > resident_max_threads(s->chain)) {  // streaming kernels: next
+        delete s;
+        return IKPSO_ERR_UNSUPPORTED;
+    }
+    *out = s;
+    return IKPSO_OK;
+}
+
+ikpso_status ikpso_solver_destroy(ikpso_solver* s)
+{
+    if (!s) return IKPSO_OK;
+    if (s->rng) (void)hipFree(s->rng);
+    delete s;
+    return IKPSO_OK;
+}
+
+ikpso_status ikpso_solver_seed(ikpso_solver* s, int64_t capacity, uint64_t seed_base, int64_t first_swarm,
+                               void* stream)
+{
+    if (!s || capacity < 0 || first_swarm < 0) return IKPSO_ERR_INVALID_ARG;
+    if (capacity > s->capacity) {
+        if (s->rng) IKPSO_HIP(hipFree(s->rng));
+        s->rng = nullptr;
+        s->capacity = 0;
+        IKPSO_HIP(hipMalloc(&s->rng, sizeof(ikpso_rng_state) * (size_t)capacity * s->P));
+        s->capacity = capacity;
+    }
+    IKPSO_HIP(launch_init_generators(s->rng, capacity * s->P, seed_base + (uint64_t)first_swarm * s->P,
+                                     (hipStream_t)stream));
+    return IKPSO_OK;
+}
+
+ikpso_status ikpso_solve_batch(ikpso_solver* s, const float* targets, const float* start_pose, int64_t num_swarms,
+                               int32_t iterations, float* out_angles, float* out_fitness, float* out_residual,
+                               void* stream)
+{
+    if (!s || num_swarms < 0 || iterations < 0) return IKPSO_ERR_INVALID_ARG;
+    if (num_swarms == 0) return IKPSO_OK;
+    if (!out_angles) return IKPSO_ERR_INVALID_ARG;  // targets == NULL: chain targets for every swarm
+    if (num_swarms > s->capacity || !s->rng) return IKPSO_ERR_INVALID_ARG;  // seed first
+    if (num_swarms > 0x7fffffff) return IKPSO_ERR_INVALID_ARG;
+    SwarmIO io{};
+    io.targets = targets;
+    io.start_pose = start_pose;
+    io.rng = s->rng;
+    io.out_angles = out_angles;
+    io.out_fitness = out_fitness;
+    io.out_residual = out_residual;
+    io.dump_particles = nullptr;
+    io.dump_bests = nullptr;
+    io.P = s->P;
+    io.iterations = iterations;
+    io.num_swarms = num_swarms;
+    IKPSO_HIP(launch_resident(s->chain, s->mode, io, (hipStream_t)stream));
+    return IKPSO_OK;
+}
+
+ikpso_status ikpso_solver_evaluate(ikpso_solver* s, const float* angles, const float* targets, const float* rest,
+                                   int64_t n, float* out_fitness, float* out_positions, void* stream)
+{
+    if (!s || n < 0 || (n > 0 && !angles)) return IKPSO_ERR_INVALID_ARG;
+    EvalIO io{angles, targets, rest, out_fitness, out_positions, n};
+    IKPSO_HIP(launch_evaluate(s->chain, s->mode, io, (hipStream_t)stream));
+    return IKPSO_OK;
+}
+
+int ikpso_solver_dof(const ikpso_solver* s) { return s ? 3 * s->chain.J : 0; }
+int ikpso_solver_effectors(const ikpso_solver* s) { return s ? s->chain.E : 0; }
+const char* ikpso_solver_kernel_name(const ikpso_solver* s) { return s ? kernel_name(s->chain) : ""; }
+
+}  // extern "C"

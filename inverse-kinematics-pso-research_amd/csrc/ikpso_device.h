@@ -1,0 +1,417 @@
+// ikpso_device.h -- device building blocks of the MI355X PSO-IK hot path.
+//
+// Everything here is written for gfx950 (CDNA4, wave64).  Reference being
+// replaced (src/ = InverseKinematicsResearch/InverseKinematicsResearch/):
+//   XORWOW generator            curand_init/curand_uniform used at src/utility_kernels.cuh:28,
+//                               src/kernel.cu:164-166,261
+//   forward kinematics          updateChainMatrices src/kernel.cu:31-62 + src/matrix_operations.cuh
+//   fitness                     calculateDistance src/kernel.cu:64-151 (collider branch excluded)
+//   velocity/position update    simulateParticlesKernel src/kernel.cu:153-189
+//   swarm argmin                thrust::min_element src/kernel.cu:297,315 (first minimum)
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "ikpso_params.h"
+
+namespace ikpso {
+
+// ---------------------------------------------------------------- XORWOW
+// cuRAND XORWOW restated: state {d, v[5]}; curand() and curand_uniform().
+struct Xorwow {
+    uint32_t d, v0, v1, v2, v3, v4;
+
+    __device__ __forceinline__ uint32_t next()
+    {
+        const uint32_t t = v0 ^ (v0 >> 2);
+        v0 = v1;
+        v1 = v2;
+        v2 = v3;
+        v3 = v4;
+        v4 = (v4 ^ (v4 << 4)) ^ (t ^ (t << 1));
+        d += 362437u;
+        return v4 + d;
+    }
+    // x * 2^-32 + 2^-33 in (0, 1]; the product is exact, so fused or not the
+    // result is the same single rounding.
+    __device__ __forceinline__ float uniform()
+    {
+        return __builtin_fmaf((float)next(), 2.3283064e-10f, 1.16415322e-10f);
+    }
+};
+
+__host__ __device__ inline void xorwow_seed(uint64_t seed, uint32_t st[6])
+{
+    const uint32_t s0 = ((uint32_t)seed) ^ 0xaad26b49u;
+    const uint32_t s1 = (uint32_t)(seed >> 32) ^ 0xf7dcefddu;
+    const uint32_t t0 = 1099087573u * s0;
+    const uint32_t t1 = 2591861531u * s1;
+    st[0] = 6615241u + t1 + t0;
+    st[1] = 123456789u + t0;
+    st[2] = 362436069u ^ t0;
+    st[3] = 521288629u + t1;
+    st[4] = 88675123u ^ t1;
+    st[5] = 5783321u + t0;
+}
+
+// ------------------------------------------------------------------ sincos
+// The particle angles are clamped to the joint limits, so |x| is small; the
+// library sincosf inlines a Payne-Hanek path for huge arguments at every call
+// site (42 sites per particle-update), which costs ~12k instructions of code
+// and spills the particle state.  Both variants below reduce |x| < 2^12 inline
+// and send anything else (or a non-finite x) to an outlined library call.
+
+__device__ __attribute__((noinline)) void sincos_slow(float x, float* s, float* c) { sincosf(x, s, c); }
+
+// FAST: Cody-Waite reduction by pi/2 with three FMA steps, then minimax
+// polynomials on [-pi/4, pi/4] (sin: odd degree 7, cos: even degree 8; about
+// 1 ulp).
+__device__ __forceinline__ void sincos_fast(float x, float* s_out, float* c_out)
+{
+    const float k = __builtin_rintf(x * 0.636619772367581343f);
+    float r = __builtin_fmaf(-k, 1.57079637050628662109375f, x);
+    r = __builtin_fmaf(-k, -4.37113900018624283e-8f, r);
+    r = __builtin_fmaf(-k, -1.71512451000591571e-15f, r);
+    const float z = r * r;
+    const float sp = __builtin_fmaf(__builtin_fmaf(-1.9515295891e-4f, z, 8.3321608736e-3f), z, -1.6666654611e-1f);
+    const float sv = __builtin_fmaf(sp * z, r, r);
+    const float cp = __builtin_fmaf(__builtin_fmaf(2.443315711809948e-5f, z, -1.388731625493765e-3f), z,
+                                    4.166664568298827e-2f);
+    const float cv = __builtin_fmaf(cp * z, z, __builtin_fmaf(-0.5f, z, 1.0f));
+    const int q = (int)k;
+    const bool swap = q & 1;
+    float sn = swap ? cv : sv;
+    float cs = swap ? sv : cv;
+    sn = (q & 2) ? -sn : sn;
+    cs = ((q + 1) & 2) ? -cs : cs;
+    *s_out = sn;
+    *c_out = cs;
+}
+
+// REFERENCE: the reduction and the polynomials (fdlibm __kernel_sin /
+// __kernel_cos coefficients) in fp64, rounded once to fp32, so the result is
+// the correctly rounded sinf/cosf except in vanishingly rare near-tie cases --
+// the same property the host libm's double-evaluated sinf/cosf has, which
+// keeps this mode in bitwise agreement with the CPU oracle.
+__device__ __forceinline__ void sincos_reference(float x, float* s_out, float* c_out)
+{
+    const float kf = __builtin_rintf(x * 0.636619772367581343f);
+    const double k = (double)kf;
+    double r = __builtin_fma(-k, 1.57079632673412561417e+00, (double)x);
+    r = __builtin_fma(-k, 6.07710050650619224932e-11, r);
+    const double z = r * r;
+    double sp = __builtin_fma(z, 1.58969099521155010221e-10, -2.50507602534068634195e-08);
+    sp = __builtin_fma(z, sp, 2.75573137070700676789e-06);
+    sp = __builtin_fma(z, sp, -1.98412698298579493134e-04);
+    sp = __builtin_fma(z, sp, 8.33333333332248946124e-03);
+    sp = __builtin_fma(z, sp, -1.66666666666666324348e-01);
+    const double sv = __builtin_fma(r * z, sp, r);
+    double cp = __builtin_fma(z, -1.13596475577881948265e-11, 2.08757232129817482790e-09);
+    cp = __builtin_fma(z, cp, -2.75573143513906633035e-07);
+    cp = __builtin_fma(z, cp, 2.48015872894767294178e-05);
+    cp = __builtin_fma(z, cp, -1.38888888888741095749e-03);
+    cp = __builtin_fma(z, cp, 4.16666666666666019037e-02);
+    const double cv = __builtin_fma(z * z, cp, __builtin_fma(-0.5, z, 1.0));
+    const int q = (int)kf;
+    const bool swap = q & 1;
+    float sn = (float)(swap ? cv : sv);
+    float cs = (float)(swap ? sv : cv);
+    sn = (q & 2) ? -sn : sn;
+    cs = ((q + 1) & 2) ? -cs : cs;
+    *s_out = sn;
+    *c_out = cs;
+}
+
+// ------------------------------------------------------------- topologies
+// The kinematic tree is a compile-time parameter so that every node frame
+// lives in registers (a runtime-indexed frame array would go to scratch) and
+// the per-node effector test is resolved at compile time.  parent(k) and
+// effector(k) for k = 1..J; node 0 is the origin.
+
+// The reference's scene (src/Main.cpp:76-116): origin -> 4 elbows -> 3 wrist
+// effectors hanging off the last elbow; DFS parent indices [-1,0,1,2,3,4,4,4].
+struct TopoRef7 {
+    static constexpr int J = 7;
+    static constexpr bool kGeneric = false;
+    __host__ __device__ static constexpr int parent(int k) { return k <= 5 ? k - 1 : 4; }
+    __host__ __device__ static constexpr bool effector(int k) { return k >= 5; }
+};
+
+// Serial chain of J joints with one tip effector (BASELINE config 5: J = 20).
+template <int J_>
+struct TopoSerialTip {
+    static constexpr int J = J_;
+    static constexpr bool kGeneric = false;
+    __host__ __device__ static constexpr int parent(int k) { return k - 1; }
+    __host__ __device__ static constexpr bool effector(int k) { return k == J_; }
+};
+
+// Any tree with J joints: parent indices read at run time (frames in scratch),
+// every node weighted by its effector weight (0 for non-effectors).
+template <int J_>
+struct TopoGeneric {
+    static constexpr int J = J_;
+    static constexpr bool kGeneric = true;
+    __host__ __device__ static constexpr int parent(int k) { return k - 1; }  // unused
+    __host__ __device__ static constexpr bool effector(int) { return true; }
+};
+
+// ------------------------------------------------------------------ frames
+// World transform of one node: rotation R (row-major 3x3) and position p.
+struct Frame {
+    float r00, r01, r02, r10, r11, r12, r20, r21, r22;
+    float px, py, pz;
+};
+
+__device__ __forceinline__ Frame origin_frame(const float* m0)
+{
+    Frame f;
+    f.r00 = m0[0]; f.r01 = m0[1]; f.r02 = m0[2];  f.px = m0[3];
+    f.r10 = m0[4]; f.r11 = m0[5]; f.r12 = m0[6];  f.py = m0[7];
+    f.r20 = m0[8]; f.r21 = m0[9]; f.r22 = m0[10]; f.pz = m0[11];
+    return f;
+}
+
+// FAST: closed-form local rotation Rx(a)Ry(b)Rz(c), then world = parent * local,
+// FMA contraction allowed.  For leaf nodes only the position is consumed and
+// the compiler drops the unused rotation entries.
+__device__ __forceinline__ Frame child_frame_fast(const Frame& P, float a, float b, float c, float len)
+{
+    float sa, ca, sb, cb, sc, cc;
+    sincos_fast(a, &sa, &ca);
+    sincos_fast(b, &sb, &cb);
+    sincos_fast(c, &sc, &cc);
+    const float p = sa * sb, q = ca * sb;
+    const float l00 = cb * cc, l01 = -cb * sc, l02 = sb;
+    const float l10 = p * cc + ca * sc, l11 = ca * cc - p * sc, l12 = -sa * cb;
+    const float l20 = sa * sc - q * cc, l21 = q * sc + sa * cc, l22 = ca * cb;
+    Frame W;
+    W.r00 = P.r00 * l00 + P.r01 * l10 + P.r02 * l20;
+    W.r01 = P.r00 * l01 + P.r01 * l11 + P.r02 * l21;
+    W.r02 = P.r00 * l02 + P.r01 * l12 + P.r02 * l22;
+    W.r10 = P.r10 * l00 + P.r11 * l10 + P.r12 * l20;
+    W.r11 = P.r10 * l01 + P.r11 * l11 + P.r12 * l21;
+    W.r12 = P.r10 * l02 + P.r11 * l12 + P.r12 * l22;
+    W.r20 = P.r20 * l00 + P.r21 * l10 + P.r22 * l20;
+    W.r21 = P.r20 * l01 + P.r21 * l11 + P.r22 * l21;
+    W.r22 = P.r20 * l02 + P.r21 * l12 + P.r22 * l22;
+    W.px = P.px + len * W.r00;
+    W.py = P.py + len * W.r10;
+    W.pz = P.pz + len * W.r20;
+    return W;
+}
+
+// REFERENCE: the exact sequence of roundings of the reference's
+// I*Rx*Ry*Rz*T(len) followed by parent*local 4x4 products
+// (src/kernel.cu:52-56, src/matrix_operations.cuh:20-38,123-180) with every
+// product by an exact 0 or 1 elided (they do not change a finite value), and
+// no FMA contraction.
+__device__ __forceinline__ Frame child_frame_reference(const Frame& P, float a, float b, float c, float len)
+{
+#pragma clang fp contract(off)
+    float sa, ca, sb, cb, sc, cc;
+    sincos_reference(a, &sa, &ca);
+    sincos_reference(b, &sb, &cb);
+    sincos_reference(c, &sc, &cc);
+    // A2 = Rx(a) * Ry(b)
+    const float a00 = cb, a02 = sb;
+    const float a10 = sa * sb, a11 = ca, a12 = (-sa) * cb;
+    const float a20 = ca * (-sb), a21 = sa, a22 = ca * cb;
+    // A3 = A2 * Rz(c)
+    const float l00 = a00 * cc, l01 = a00 * (-sc), l02 = a02;
+    const float l10 = a10 * cc + a11 * sc, l11 = a10 * (-sc) + a11 * cc, l12 = a12;
+    const float l20 = a20 * cc + a21 * sc, l21 = a20 * (-sc) + a21 * cc, l22 = a22;
+    // * T(len, 0, 0): translation column = first column * len
+    const float t0 = l00 * len, t1 = l10 * len, t2 = l20 * len;
+    Frame W;
+    W.r00 = P.r00 * l00 + P.r01 * l10 + P.r02 * l20;
+    W.r01 = P.r00 * l01 + P.r01 * l11 + P.r02 * l21;
+    W.r02 = P.r00 * l02 + P.r01 * l12 + P.r02 * l22;
+    W.r10 = P.r10 * l00 + P.r11 * l10 + P.r12 * l20;
+    W.r11 = P.r10 * l01 + P.r11 * l11 + P.r12 * l21;
+    W.r12 = P.r10 * l02 + P.r11 * l12 + P.r12 * l22;
+    W.r20 = P.r20 * l00 + P.r21 * l10 + P.r22 * l20;
+    W.r21 = P.r20 * l01 + P.r21 * l11 + P.r22 * l21;
+    W.r22 = P.r20 * l02 + P.r21 * l12 + P.r22 * l22;
+    W.px = P.r00 * t0 + P.r01 * t1 + P.r02 * t2 + P.px;
+    W.py = P.r10 * t0 + P.r11 * t1 + P.r12 * t2 + P.py;
+    W.pz = P.r20 * t0 + P.r21 * t1 + P.r22 * t2 + P.pz;
+    return W;
+}
+
+template <int MODE>
+__device__ __forceinline__ Frame child_frame(const Frame& P, float a, float b, float c, float len)
+{
+    if constexpr (MODE == IKPSO_ARITH_REFERENCE)
+        return child_frame_reference(P, a, b, c, len);
+    else
+        return child_frame_fast(P, a, b, c, len);
+}
+
+// ---------------------------------------------------------------- fitness
+// calculateDistance (src/kernel.cu:64-151) for one particle:
+//   f = sum_eff w_e |p_e - t_e|^2 + (dw/J) sum_k |(p_k,1) - posref_k|^2
+//       + (aw/J) sum_k |rest_k - x_k|^2   [+ soft joint-limit penalty, extension]
+// Accumulation order follows the reference (node order; (x^2+y^2)+z^2).
+// `tgt` holds the effector targets per node (3 floats at 3*(k-1)); for the
+// generic topology non-effector nodes carry weight 0 and target 0, and adding
+// the resulting +0 leaves a finite sum unchanged bit for bit.
+// POSREF: 0 = distance term off (distanceWeight == 0), 1 = on, 2 = runtime flag.
+template <class Topo, int MODE, int POSREF>
+__device__ __forceinline__ float fitness(const ChainConsts<Topo::J>& cc, const float* x, const float* rest,
+                                         const float* tgt, float* node_pos /* [3J] or nullptr */)
+{
+#pragma clang fp contract(off)
+    constexpr int J = Topo::J;
+    Frame F[J + 1];
+    F[0] = origin_frame(cc.m0);
+    float rot_diff = 0.0f, pos_diff = 0.0f, distance = 0.0f;
+    const bool posref = POSREF == 1 || (POSREF == 2 && cc.use_posref);
+#pragma unroll
+    for (int k = 1; k <= J; ++k) {
+        const int pk = Topo::kGeneric ? cc.parent[k] : Topo::parent(k);
+        const float a = x[3 * (k - 1) + 0], b = x[3 * (k - 1) + 1], c = x[3 * (k - 1) + 2];
+        F[k] = child_frame<MODE>(F[pk], a, b, c, cc.len[k]);
+        const float dx = rest[3 * (k - 1) + 0] - a, dy = rest[3 * (k - 1) + 1] - b, dz = rest[3 * (k - 1) + 2] - c;
+        if constexpr (MODE == IKPSO_ARITH_REFERENCE) {
+            rot_diff = rot_diff + ((dx * dx + dy * dy) + dz * dz);
+        } else {
+#pragma clang fp contract(fast)
+            rot_diff = rot_diff + ((dx * dx + dy * dy) + dz * dz);
+        }
+        if (posref) {  // distance_weight != 0
+            const float* pr = cc.aux + 4 * (k - 1);  // positions[(k-1)*4 ..] (src/kernel.cu:94-98)
+            const float ex = F[k].px - pr[0];
+            const float ey = F[k].py - pr[1];
+            const float ez = F[k].pz - pr[2];
+            const float ew = 1.0f - pr[3];
+            pos_diff += ((ex * ex + ey * ey) + ez * ez) + ew * ew;
+        }
+        if (Topo::effector(k)) {
+            const float ex = F[k].px - tgt[3 * (k - 1) + 0];
+            const float ey = F[k].py - tgt[3 * (k - 1) + 1];
+            const float ez = F[k].pz - tgt[3 * (k - 1) + 2];
+            if constexpr (MODE == IKPSO_ARITH_REFERENCE) {
+                distance = distance + ((ex * ex + ey * ey) + ez * ez) * cc.eff_w[k];
+            } else {
+#pragma clang fp contract(fast)
+                distance = distance + ((ex * ex + ey * ey) + ez * ez) * cc.eff_w[k];
+            }
+        }
+        if (node_pos) {
+            node_pos[3 * (k - 1) + 0] = F[k].px;
+            node_pos[3 * (k - 1) + 1] = F[k].py;
+            node_pos[3 * (k - 1) + 2] = F[k].pz;
+        }
+        // One node at a time: without this the scheduler hoists all 3J
+        // independent sincos evaluations to the top and spills the state.
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    float f = posref ? (distance + cc.dw_j * pos_diff) + cc.aw_j * rot_diff : distance + cc.aw_j * rot_diff;
+    if (cc.use_penalty) {  // soft joint-limit penalty (extension, BASELINE config 5)
+        float pen = 0.0f;
+#pragma unroll
+        for (int d = 0; d < 3 * J; ++d) {
+            const float slo = cc.aux[4 * J + d], shi = cc.aux[7 * J + d];
+            const float over = fmaxf(fmaxf(x[d] - shi, slo - x[d]), 0.0f);
+            pen = pen + over * over;
+        }
+        f = f + cc.lim_w * pen;
+    }
+    return f;
+}
+
+// Sum over effectors of the Euclidean distance to target (checkDistance,
+// src/Main.cpp:290-298 / src/Node.h:421-429), evaluated with the device FK.
+template <class Topo, int MODE>
+__device__ __forceinline__ float residual(const ChainConsts<Topo::J>& cc, const float* x, const float* tgt)
+{
+    constexpr int J = Topo::J;
+    Frame F[J + 1];
+    F[0] = origin_frame(cc.m0);
+    float r = 0.0f;
+#pragma unroll
+    for (int k = 1; k <= J; ++k) {
+        const int pk = Topo::kGeneric ? cc.parent[k] : Topo::parent(k);
+        F[k] = child_frame<MODE>(F[pk], x[3 * (k - 1)], x[3 * (k - 1) + 1], x[3 * (k - 1) + 2], cc.len[k]);
+        if (Topo::effector(k) && cc.eff_slot[k] >= 0) {
+            const float dx = tgt[3 * (k - 1) + 0] - F[k].px;
+            const float dy = tgt[3 * (k - 1) + 1] - F[k].py;
+            const float dz = tgt[3 * (k - 1) + 2] - F[k].pz;
+            r += sqrtf(dx * dx + dy * dy + dz * dz);
+        }
+    }
+    return r;
+}
+
+// ------------------------------------------------------------ PSO update
+// simulateParticlesKernel body for one dimension (src/kernel.cu:160-169):
+//   v = w*r1*v + c1*r2*(pb - x) + c2*r3*(g - x);  x += v
+template <int MODE>
+__device__ __forceinline__ void pso_update(float& x, float& v, float pb, float g, float w, float c1, float c2,
+                                           Xorwow& rng)
+{
+    const float r1 = rng.uniform();
+    const float r2 = rng.uniform();
+    const float r3 = rng.uniform();
+    if constexpr (MODE == IKPSO_ARITH_REFERENCE) {
+#pragma clang fp contract(off)
+        v = w * r1 * v + c1 * r2 * (pb - x) + c2 * r3 * (g - x);
+        x += v;
+    } else {
+#pragma clang fp contract(fast)
+        v = w * r1 * v + c1 * r2 * (pb - x) + c2 * r3 * (g - x);
+        x += v;
+    }
+}
+
+// clamp (src/matrix_operations.cuh:187-190)
+__device__ __forceinline__ float clamp_ref(float v, float lo, float hi) { return fminf(fmaxf(v, lo), hi); }
+
+// ------------------------------------------------------------- reductions
+// Order-preserving map of an fp32 value to uint32 (-0 canonicalised to +0) so
+// that an unsigned min is a float min; ties then break to the lowest index,
+// as thrust::min_element does.
+__device__ __forceinline__ uint32_t ordered_key(float f)
+{
+    const uint32_t u = __float_as_uint(f + 0.0f);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__host__ __device__ inline float key_to_float(uint32_t k)
+{
+    const uint32_t u = (k & 0x80000000u) ? (k & 0x7fffffffu) : ~k;
+    float f;
+    __builtin_memcpy(&f, &u, 4);
+    return f;
+}
+
+// Wave64 unsigned min, result uniform: DPP within each 16-lane row
+// (quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror, row_mirror), then the
+// four row minima through readlane on the scalar unit.
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t x)
+{
+    x = min(x, (uint32_t)__builtin_amdgcn_update_dpp((int)0xFFFFFFFF, (int)x, 0xB1, 0xF, 0xF, false));
+    x = min(x, (uint32_t)__builtin_amdgcn_update_dpp((int)0xFFFFFFFF, (int)x, 0x4E, 0xF, 0xF, false));
+    x = min(x, (uint32_t)__builtin_amdgcn_update_dpp((int)0xFFFFFFFF, (int)x, 0x141, 0xF, 0xF, false));
+    x = min(x, (uint32_t)__builtin_amdgcn_update_dpp((int)0xFFFFFFFF, (int)x, 0x140, 0xF, 0xF, false));
+    const uint32_t r0 = (uint32_t)__builtin_amdgcn_readlane((int)x, 0);
+    const uint32_t r1 = (uint32_t)__builtin_amdgcn_readlane((int)x, 16);
+    const uint32_t r2 = (uint32_t)__builtin_amdgcn_readlane((int)x, 32);
+    const uint32_t r3 = (uint32_t)__builtin_amdgcn_readlane((int)x, 48);
+    return min(min(r0, r1), min(r2, r3));
+}
+
+// Lowest lane whose key equals the (uniform) wave minimum.
+__device__ __forceinline__ int wave_first_lane_eq(uint32_t key, uint32_t wmin)
+{
+    const uint64_t m = __ballot(key == wmin);
+    return (int)__builtin_ctzll(m);
+}
+
+__device__ __forceinline__ float uniform_f32(float v)
+{
+    return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
+}
+
+}  // namespace ikpso

@@ -1,0 +1,91 @@
+// ikpso_kernels.h -- host-side view of the kernel library: the parsed chain,
+// launch entry points and their parameter blocks.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <string.h>
+
+#include <vector>
+
+#include "ikpso.h"
+#include "ikpso_params.h"
+
+namespace ikpso {
+
+// Ref7: the reference scene's tree with effectors on nodes 5..7; SerialTip:
+// serial chain with a single tip effector; Generic: anything else.
+enum class TopoKind { Ref7, SerialTip, Generic };
+
+// The chain as the kernels need it, parsed once from the caller's node table.
+struct ChainHost {
+    int J = 0;  // joints = node_count - 1
+    int E = 0;  // effectors
+    TopoKind topo = TopoKind::Generic;
+    std::vector<int> parent, eff_slot;
+    std::vector<float> len, eff_w, lo, hi, rest, tgt0;
+    std::vector<float> aux;          // [posref 4J | soft_lo 3J | soft_hi 3J] (host copy)
+    const float* aux_dev = nullptr;  // device copy, owned by the solver / call
+    float m0[12] = {};
+    float w = 0, c1 = 0, c2 = 0, aw_j = 0, dw_j = 0, lim_w = 0;
+    bool use_posref = false, use_penalty = false;
+};
+
+// Evaluate-kernel parameters.
+struct EvalIO {
+    const float* angles;   // [n][D]
+    const float* targets;  // [n][E][3] or null (chain targets)
+    const float* rest;     // [n][D] or null (chain rotations)
+    float* out_fitness;    // [n] or null
+    float* out_positions;  // [n][J][3] or null
+    int64_t n;
+};
+
+// Threads per workgroup the resident kernel is compiled for: 1024 lanes
+// (16 waves, 4 per SIMD, <= 128 VGPRs) while x/v/pbest of one particle fit,
+// 256 lanes (one wave per SIMD, up to 512 VGPRs) for long chains.
+template <int J>
+__host__ __device__ constexpr int kResidentMaxThreads()
+{
+    return J <= 10 ? 1024 : 256;
+}
+
+template <int J>
+ChainConsts<J> make_consts(const ChainHost& h)
+{
+    ChainConsts<J> c;
+    memset(&c, 0, sizeof(c));
+    for (int k = 0; k <= J; ++k) {
+        c.len[k] = h.len[k];
+        c.eff_w[k] = h.eff_w[k];
+        c.eff_slot[k] = h.eff_slot[k];
+        c.parent[k] = h.parent[k];
+    }
+    for (int d = 0; d < 3 * J; ++d) {
+        c.lo[d] = h.lo[d];
+        c.hi[d] = h.hi[d];
+        c.rest[d] = h.rest[d];
+        c.tgt0[d] = h.tgt0[d];
+    }
+    for (int i = 0; i < 12; ++i) c.m0[i] = h.m0[i];
+    c.aux = h.aux_dev;
+    c.w = h.w;
+    c.c1 = h.c1;
+    c.c2 = h.c2;
+    c.aw_j = h.aw_j;
+    c.dw_j = h.dw_j;
+    c.lim_w = h.lim_w;
+    c.use_posref = h.use_posref ? 1 : 0;
+    c.use_penalty = h.use_penalty ? 1 : 0;
+    c.num_eff = h.E;
+    return c;
+}
+
+hipError_t launch_init_generators(ikpso_rng_state* st, int64_t count, uint64_t seed_base, hipStream_t stream);
+hipError_t launch_resident(const ChainHost& ch, int mode, const SwarmIO& io, hipStream_t stream);
+hipError_t launch_evaluate(const ChainHost& ch, int mode, const EvalIO& io, hipStream_t stream);
+int resident_max_threads(const ChainHost& ch);
+bool chain_supported(const ChainHost& ch);
+const char* kernel_name(const ChainHost& ch);
+
+}  // namespace ikpso

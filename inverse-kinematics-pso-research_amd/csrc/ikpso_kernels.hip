@@ -1,0 +1,379 @@
+// ikpso_kernels.hip -- gfx950 kernels of the PSO inverse-kinematics hot path.
+//
+// Replaces the reference's per-iteration launch chain (src/kernel.cu:279-327:
+// initParticlesKernel, initLocalBests, thrust::min_element, a blocking D2H
+// copy and updateGlobalBestCoordsKernel per iteration) with ONE launch per
+// batch of swarms:
+//
+//   k_swarm_resident: one workgroup = one swarm, one lane = one particle
+//     (P <= 1024).  Position, velocity, local best, local-best fitness and the
+//     XORWOW state of a particle stay in VGPRs for all iterations; the chain
+//     constants sit in the kernarg segment (scalar loads); the swarm argmin is
+//     a DPP wave64 min + ballot, then one 16-entry LDS pass; the global-best
+//     vector is broadcast through LDS only when it strictly improves (the
+//     `globalMin > currentGlobalMin` test of src/kernel.cu:318).  HBM traffic
+//     is the RNG state in/out and the outputs: the kernel is VALU-bound.
+//
+//   k_init_generators: curand_init(seed_base + i, 0, 0) per state
+//     (randInitKernel, src/utility_kernels.cuh:21-31).
+//
+//   k_evaluate: FK + fitness of given angle vectors (parity/KAT entry).
+#include <hip/hip_runtime.h>
+
+#include "ikpso_device.h"
+#include "ikpso_kernels.h"
+
+namespace ikpso {
+
+// ------------------------------------------------------------------ RNG init
+__global__ void __launch_bounds__(256) k_init_generators(ikpso_rng_state* st, int64_t count, uint64_t seed_base)
+{
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < count;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        uint32_t s[6];
+        xorwow_seed(seed_base + (uint64_t)i, s);
+        ikpso_rng_state r;
+        r.d = s[0];
+        r.v[0] = s[1];
+        r.v[1] = s[2];
+        r.v[2] = s[3];
+        r.v[3] = s[4];
+        r.v[4] = s[5];
+        r.boxmuller_flag = 0;
+        r.boxmuller_flag_double = 0;
+        r.boxmuller_extra = 0.0f;
+        r.pad_ = 0;
+        r.boxmuller_extra_double = 0.0;
+        st[i] = r;
+    }
+}
+
+// Seeds swarm-major states: state (b, i) = curand_init(seed_base + (first_swarm + b) * P + i).
+// With a contiguous swarm range this is seed_base + first_swarm * P + flat index.
+hipError_t launch_init_generators(ikpso_rng_state* st, int64_t count, uint64_t seed_base, hipStream_t stream)
+{
+    if (count <= 0) return hipSuccess;
+    int64_t blocks = (count + 255) / 256;
+    if (blocks > 65536) blocks = 65536;
+    hipLaunchKernelGGL(k_init_generators, dim3((unsigned)blocks), dim3(256), 0, stream, st, count, seed_base);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------- resident swarm kernel
+__device__ __forceinline__ void load_rng(Xorwow& r, const ikpso_rng_state* p)
+{
+    const uint32_t* q = reinterpret_cast<const uint32_t*>(p);
+    r.d = q[0];
+    r.v0 = q[1];
+    r.v1 = q[2];
+    r.v2 = q[3];
+    r.v3 = q[4];
+    r.v4 = q[5];
+}
+
+__device__ __forceinline__ void store_rng(const Xorwow& r, ikpso_rng_state* p)
+{
+    uint32_t* q = reinterpret_cast<uint32_t*>(p);
+    q[0] = r.d;
+    q[1] = r.v0;
+    q[2] = r.v1;
+    q[3] = r.v2;
+    q[4] = r.v3;
+    q[5] = r.v4;
+}
+
+// Per-swarm uniform constants staged in LDS.  They are read at their point of
+// use every iteration (an empty asm with a memory clobber at the top of the
+// iteration stops the compiler from hoisting them into registers): ~100
+// loop-invariant uniforms held in SGPRs/VGPRs across the loop spill, while a
+// broadcast ds_read costs one LDS cycle.
+template <int J>
+struct SwarmShared {
+    float lo[3 * J], hi[3 * J];  // clamp bounds
+    float rest[3 * J];           // warm start + angle-term reference
+    float tgt[3 * J];            // effector targets per node (k-1), 0 elsewhere
+    float g[3 * J];              // global-best vector
+    uint32_t key[2][16];         // per-wave argmin, double-buffered by parity
+    int32_t idx[2][16];
+};
+
+template <int J>
+__device__ __forceinline__ void stage_swarm_inputs(const ChainConsts<J>& cc, const SwarmIO& io, int64_t b,
+                                                   SwarmShared<J>& sh)
+{
+    constexpr int D = 3 * J;
+    const float* t = io.targets ? io.targets + b * (int64_t)cc.num_eff * 3 : nullptr;
+    for (int d = threadIdx.x; d < D; d += blockDim.x) {
+        sh.lo[d] = cc.lo[d];
+        sh.hi[d] = cc.hi[d];
+        sh.rest[d] = io.start_pose ? io.start_pose[b * D + d] : cc.rest[d];
+        const int s = cc.eff_slot[d / 3 + 1];
+        sh.tgt[d] = t ? (s >= 0 ? t[3 * s + d % 3] : 0.0f) : cc.tgt0[d];
+    }
+}
+
+__device__ __forceinline__ void compiler_fence() { asm volatile("" ::: "memory"); }
+
+// Swarm argmin of the local-best fitness keys, lowest particle index on ties
+// (thrust::min_element, src/kernel.cu:297,315).  One DPP wave min + ballot per
+// wave, a 16-entry LDS exchange, then every wave reduces the 16 entries
+// redundantly, so the result is uniform without a second barrier.
+template <int J>
+__device__ __forceinline__ uint32_t swarm_argmin(SwarmShared<J>& sh, int par, uint32_t key, int* out_idx)
+{
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int nwaves = blockDim.x >> 6;
+    const uint32_t wmin = wave_min_u32(key);
+    if (lane == wave_first_lane_eq(key, wmin)) {
+        sh.key[par][wave] = wmin;
+        sh.idx[par][wave] = tid;
+    }
+    __syncthreads();
+    const uint32_t k2 = lane < nwaves ? sh.key[par][lane] : 0xFFFFFFFFu;
+    const uint32_t bmin = wave_min_u32(k2);
+    *out_idx = sh.idx[par][wave_first_lane_eq(k2, bmin)];
+    return bmin;
+}
+
+template <class Topo, int MODE, int POSREF>
+__global__ void __launch_bounds__(kResidentMaxThreads<Topo::J>())
+    k_swarm_resident(const ChainConsts<Topo::J> cc, const SwarmIO io)
+{
+    constexpr int J = Topo::J;
+    constexpr int D = 3 * J;
+    constexpr int BLOCK = kResidentMaxThreads<J>();
+    const int64_t b = blockIdx.x;
+    const int tid = threadIdx.x;
+    const int P = io.P;
+    const bool active = tid < P;
+
+    __shared__ SwarmShared<J> sh;
+    // Local-best positions, [d][lane]: read once per iteration by the update,
+    // written on improvement; consecutive lanes hit consecutive banks.
+    __shared__ float s_pb[D * BLOCK];
+    stage_swarm_inputs<J>(cc, io, b, sh);
+
+    Xorwow rng{0, 0, 0, 0, 0, 0};
+    if (active) load_rng(rng, io.rng + b * P + tid);
+    __syncthreads();
+
+    // initParticlesKernel (src/kernel.cu:223-266): warm start at the current
+    // pose, v = U*2-1 (D draws in dimension order), pbest = x.
+    float x[D], v[D];
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+        x[d] = sh.rest[d];
+        v[d] = __builtin_fmaf(rng.uniform(), 2.0f, -1.0f);
+        s_pb[d * BLOCK + tid] = x[d];
+    }
+    // initLocalBests (src/kernel.cu:191-200)
+    float pbf = fitness<Topo, MODE, POSREF>(cc, x, sh.rest, sh.tgt, nullptr);
+
+    // swarm argmin + unconditional first global-best copy (src/kernel.cu:297-304)
+    int bidx;
+    uint32_t gkey = swarm_argmin<J>(sh, 0, active ? ordered_key(pbf) : 0xFFFFFFFFu, &bidx);
+    if (tid < D) sh.g[tid] = s_pb[tid * BLOCK + bidx];
+    __syncthreads();
+
+    const float w = cc.w, c1 = cc.c1, c2 = cc.c2;
+    for (int it = 0; it < io.iterations; ++it) {
+        compiler_fence();
+        // simulateParticlesKernel (src/kernel.cu:153-189)
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            pso_update<MODE>(x[d], v[d], s_pb[d * BLOCK + tid], sh.g[d], w, c1, c2, rng);
+            if (d % 3 == 2) __builtin_amdgcn_sched_barrier(0);
+        }
+#pragma unroll
+        for (int d = 0; d < D; ++d) x[d] = clamp_ref(x[d], sh.lo[d], sh.hi[d]);
+
+        // updateLocalBests (src/kernel.cu:202-221): strict improvement
+        const float f = fitness<Topo, MODE, POSREF>(cc, x, sh.rest, sh.tgt, nullptr);
+        if (f < pbf) {
+            pbf = f;
+#pragma unroll
+            for (int d = 0; d < D; ++d) s_pb[d * BLOCK + tid] = x[d];
+        }
+
+        // thrust::min_element + `globalMin > currentGlobalMin` (src/kernel.cu:315-323)
+        const uint32_t bmin = swarm_argmin<J>(sh, (it + 1) & 1, active ? ordered_key(pbf) : 0xFFFFFFFFu, &bidx);
+        if (bmin < gkey) {  // uniform across the workgroup
+            gkey = bmin;
+            if (tid < D) sh.g[tid] = s_pb[tid * BLOCK + bidx];
+            __syncthreads();
+        }
+    }
+
+    // outputs: Coordinates result (updateGlobalBestCoordsKernel) + fitness + residual
+    compiler_fence();
+    if (tid < D) io.out_angles[b * D + tid] = sh.g[tid];
+    if (tid == 0 && io.out_fitness) io.out_fitness[b] = key_to_float(gkey);
+    if (io.out_residual && tid < 64) {
+        float g[D];
+#pragma unroll
+        for (int d = 0; d < D; ++d) g[d] = sh.g[d];
+        const float r = residual<Topo, MODE>(cc, g, sh.tgt);
+        if (tid == 0) io.out_residual[b] = r;
+    }
+    if (active) {
+        store_rng(rng, io.rng + b * P + tid);
+        if (io.dump_particles) {  // reference particles layout [3][D][P] per swarm
+            float* base = io.dump_particles + b * (int64_t)3 * D * P;
+#pragma unroll
+            for (int d = 0; d < D; ++d) {
+                base[(int64_t)d * P + tid] = x[d];
+                base[(int64_t)(D + d) * P + tid] = v[d];
+                base[(int64_t)(2 * D + d) * P + tid] = s_pb[d * BLOCK + tid];
+            }
+        }
+        if (io.dump_bests) io.dump_bests[b * P + tid] = pbf;
+    }
+}
+
+// ----------------------------------------------------------- evaluate kernel
+template <class Topo, int MODE>
+__global__ void __launch_bounds__(256) k_evaluate(const ChainConsts<Topo::J> cc, EvalIO io)
+{
+    constexpr int J = Topo::J;
+    constexpr int D = 3 * J;
+    for (int64_t n = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; n < io.n;
+         n += (int64_t)gridDim.x * blockDim.x) {
+        float x[D], rest[D], tgt[D], pos[D];
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            x[d] = io.angles[n * D + d];
+            rest[d] = io.rest ? io.rest[n * D + d] : cc.rest[d];
+        }
+        if (io.targets) {
+#pragma unroll
+            for (int k = 1; k <= J; ++k) {
+                const int s = cc.eff_slot[k];
+#pragma unroll
+                for (int c = 0; c < 3; ++c)
+                    tgt[3 * (k - 1) + c] = s >= 0 ? io.targets[(n * cc.num_eff + s) * 3 + c] : 0.0f;
+            }
+        } else {
+#pragma unroll
+            for (int d = 0; d < D; ++d) tgt[d] = cc.tgt0[d];
+        }
+        const float f = fitness<Topo, MODE, 2>(cc, x, rest, tgt, pos);
+        if (io.out_fitness) io.out_fitness[n] = f;
+        if (io.out_positions) {
+#pragma unroll
+            for (int d = 0; d < D; ++d) io.out_positions[n * D + d] = pos[d];
+        }
+    }
+}
+
+// --------------------------------------------------------------- dispatch
+template <class Topo, int MODE>
+static hipError_t run_resident(const ChainHost& ch, const SwarmIO& io, int block, hipStream_t stream)
+{
+    const ChainConsts<Topo::J> cc = make_consts<Topo::J>(ch);
+    const dim3 grid((unsigned)io.num_swarms), threads(block);
+    if constexpr (Topo::kGeneric) {
+        hipLaunchKernelGGL((k_swarm_resident<Topo, MODE, 2>), grid, threads, 0, stream, cc, io);
+    } else {
+        if (ch.use_posref)
+            hipLaunchKernelGGL((k_swarm_resident<Topo, MODE, 1>), grid, threads, 0, stream, cc, io);
+        else
+            hipLaunchKernelGGL((k_swarm_resident<Topo, MODE, 0>), grid, threads, 0, stream, cc, io);
+    }
+    return hipGetLastError();
+}
+
+template <class Topo, int MODE>
+static hipError_t run_evaluate(const ChainHost& ch, const EvalIO& io, hipStream_t stream)
+{
+    const ChainConsts<Topo::J> cc = make_consts<Topo::J>(ch);
+    int64_t blocks = (io.n + 255) / 256;
+    if (blocks > 8192) blocks = 8192;
+    if (blocks < 1) blocks = 1;
+    hipLaunchKernelGGL((k_evaluate<Topo, MODE>), dim3((unsigned)blocks), dim3(256), 0, stream, cc, io);
+    return hipGetLastError();
+}
+
+// Visit the kernel instantiation for (topology, J, mode).  Returns false when
+// the chain has no compiled variant.
+template <class F>
+static bool visit_topology(const ChainHost& ch, F&& f)
+{
+    switch (ch.topo) {
+    case TopoKind::Ref7:
+        f(TopoRef7{});
+        return true;
+#ifndef IKPSO_EXPERIMENT_REF7_ONLY
+    case TopoKind::SerialTip:
+        switch (ch.J) {
+        case 20: f(TopoSerialTip<20>{}); return true;
+        default: break;
+        }
+        [[fallthrough]];
+    case TopoKind::Generic:
+        switch (ch.J) {
+#define IKPSO_G(n) \
+    case n: f(TopoGeneric<n>{}); return true;
+            IKPSO_G(1) IKPSO_G(2) IKPSO_G(3) IKPSO_G(4) IKPSO_G(5) IKPSO_G(6) IKPSO_G(7) IKPSO_G(8) IKPSO_G(9)
+                IKPSO_G(10) IKPSO_G(12) IKPSO_G(16) IKPSO_G(20)
+#undef IKPSO_G
+        default: return false;
+        }
+#else
+    default: return false;
+#endif
+    }
+    return false;
+}
+
+int resident_max_threads(const ChainHost& ch)
+{
+    int r = 0;
+    visit_topology(ch, [&](auto topo) { r = kResidentMaxThreads<decltype(topo)::J>(); });
+    return r;
+}
+
+bool chain_supported(const ChainHost& ch)
+{
+    return visit_topology(ch, [](auto) {});
+}
+
+const char* kernel_name(const ChainHost& ch)
+{
+    switch (ch.topo) {
+    case TopoKind::Ref7: return "swarm_resident<ref_tree7>";
+    case TopoKind::SerialTip:
+        return ch.J == 20 ? "swarm_resident<serial_tip20>" : "swarm_resident<generic>";
+    default: return "swarm_resident<generic>";
+    }
+}
+
+hipError_t launch_resident(const ChainHost& ch, int mode, const SwarmIO& io, hipStream_t stream)
+{
+    if (io.num_swarms <= 0) return hipSuccess;
+    const int block = ((io.P + 63) / 64) * 64;
+    hipError_t err = hipErrorInvalidValue;
+    const bool ok = visit_topology(ch, [&](auto topo) {
+        using T = decltype(topo);
+        if (mode == IKPSO_ARITH_REFERENCE)
+            err = run_resident<T, IKPSO_ARITH_REFERENCE>(ch, io, block, stream);
+        else
+            err = run_resident<T, IKPSO_ARITH_FAST>(ch, io, block, stream);
+    });
+    return ok ? err : hipErrorInvalidValue;
+}
+
+hipError_t launch_evaluate(const ChainHost& ch, int mode, const EvalIO& io, hipStream_t stream)
+{
+    if (io.n <= 0) return hipSuccess;
+    hipError_t err = hipErrorInvalidValue;
+    const bool ok = visit_topology(ch, [&](auto topo) {
+        using T = decltype(topo);
+        if (mode == IKPSO_ARITH_REFERENCE)
+            err = run_evaluate<T, IKPSO_ARITH_REFERENCE>(ch, io, stream);
+        else
+            err = run_evaluate<T, IKPSO_ARITH_FAST>(ch, io, stream);
+    });
+    return ok ? err : hipErrorInvalidValue;
+}
+
+}  // namespace ikpso

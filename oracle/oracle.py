@@ -1,0 +1,171 @@
+"""ctypes wrapper of the CPU oracle (oracle/ikpso_oracle.c).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg, as the checker / CPU baseline.  The product
+package never imports it.  Parity status: the oracle is pinned by the
+reference's own recorded data (Documentation/results.xlsx FK rows and
+convergence distances, tests/golden/) and its XORWOW step by rocRAND's
+xorwow_engine; the cuRAND seeding constants are spec-pinned.
+"""
+from __future__ import annotations
+
+import ctypes
+import subprocess
+from pathlib import Path
+
+import numpy as np
+
+HERE = Path(__file__).resolve().parent
+LIB_PATH = HERE / "_build" / "libikpso_oracle.so"
+
+NODE_DTYPE = np.dtype(
+    [
+        ("node_type", "<i4"), ("parent_index", "<i4"), ("effector_weight", "<f4"), ("position", "<f4", (3,)),
+        ("rotation", "<f4", (3,)), ("max_rotation", "<f4", (3,)), ("min_rotation", "<f4", (3,)),
+        ("length", "<f4"), ("target_position", "<f4", (3,)), ("target_rotation", "<f4", (3,)),
+    ]
+)
+RNG_DTYPE = np.dtype(
+    [
+        ("d", "<u4"), ("v", "<u4", (5,)), ("boxmuller_flag", "<i4"), ("boxmuller_flag_double", "<i4"),
+        ("boxmuller_extra", "<f4"), ("pad_", "<u4"), ("boxmuller_extra_double", "<f8"),
+    ]
+)
+
+_LIB = None
+_P = ctypes.c_void_p
+
+
+def build() -> Path:
+    subprocess.run(["make", "-s", "-C", str(HERE)], check=True)
+    return LIB_PATH
+
+
+def load():
+    global _LIB
+    if _LIB is None:
+        if not LIB_PATH.exists():
+            build()
+        lib = ctypes.CDLL(str(LIB_PATH))
+        sig = {
+            "orc_sizeof_rng": (ctypes.c_int, []),
+            "orc_sizeof_node": (ctypes.c_int, []),
+            "orc_curand_init": (None, [ctypes.c_uint64, _P]),
+            "orc_curand": (ctypes.c_uint32, [_P]),
+            "orc_curand_uniform": (ctypes.c_float, [_P]),
+            "orc_init_generators": (None, [_P, ctypes.c_int64, ctypes.c_uint64]),
+            "orc_uniform_stream": (None, [_P, _P, ctypes.c_int]),
+            "orc_chain_matrices": (None, [_P, ctypes.c_int, _P, _P]),
+            "orc_fitness": (ctypes.c_float, [_P, ctypes.c_int, _P, _P, ctypes.c_float, ctypes.c_float]),
+            "orc_node_positions": (None, [_P, ctypes.c_int, _P, _P]),
+            "orc_residual": (ctypes.c_float, [_P, ctypes.c_int, _P]),
+            "orc_calculate_pso": (
+                ctypes.c_int,
+                [_P, _P, _P, _P, ctypes.c_int64, _P, ctypes.c_int, ctypes.c_float, ctypes.c_float, ctypes.c_float,
+                 ctypes.c_int, ctypes.c_float, ctypes.c_float, _P],
+            ),
+            "orc_solve_batch": (
+                ctypes.c_int,
+                [_P, ctypes.c_int, _P, _P, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_float,
+                 ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float, _P, _P, _P, _P, _P, ctypes.c_int],
+            ),
+        }
+        for name, (res, args) in sig.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        assert lib.orc_sizeof_rng() == 48 and lib.orc_sizeof_node() == 88
+        _LIB = lib
+    return _LIB
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data
+
+
+def _chain(chain) -> np.ndarray:
+    c = np.ascontiguousarray(chain)
+    return c.view(NODE_DTYPE) if c.dtype != NODE_DTYPE else c
+
+
+def init_generators(count: int, seed_base: int = 0) -> np.ndarray:
+    st = np.zeros(count, dtype=RNG_DTYPE)
+    load().orc_init_generators(_p(st), int(count), int(seed_base))
+    return st
+
+
+def uniform_stream(state: np.ndarray, n: int) -> np.ndarray:
+    """Draw n curand_uniform values from one state (advances it in place)."""
+    out = np.empty(n, dtype=np.float32)
+    load().orc_uniform_stream(state.ctypes.data, _p(out), int(n))
+    return out
+
+
+def raw_stream(state: np.ndarray, n: int) -> np.ndarray:
+    lib = load()
+    return np.array([lib.orc_curand(state.ctypes.data) for _ in range(n)], dtype=np.uint32)
+
+
+def chain_matrices(chain, angles) -> np.ndarray:
+    c = _chain(chain)
+    a = np.ascontiguousarray(angles, dtype=np.float32)
+    out = np.empty((c.shape[0], 4, 4), dtype=np.float32)
+    load().orc_chain_matrices(_p(c), c.shape[0], _p(a), _p(out))
+    return out
+
+
+def node_positions(chain, angles) -> np.ndarray:
+    c = _chain(chain)
+    a = np.ascontiguousarray(angles, dtype=np.float32)
+    out = np.empty((c.shape[0] - 1, 3), dtype=np.float32)
+    load().orc_node_positions(_p(c), c.shape[0], _p(a), _p(out))
+    return out
+
+
+def fitness(chain, angles, angle_weight=3.0, distance_weight=0.0, positions=None) -> np.float32:
+    c = _chain(chain)
+    a = np.ascontiguousarray(angles, dtype=np.float32)
+    pos = None if positions is None else np.ascontiguousarray(positions, dtype=np.float32)
+    return np.float32(load().orc_fitness(_p(c), c.shape[0], _p(pos), _p(a), angle_weight, distance_weight))
+
+
+def residual(chain, angles) -> np.float32:
+    c = _chain(chain)
+    a = np.ascontiguousarray(angles, dtype=np.float32)
+    return np.float32(load().orc_residual(_p(c), c.shape[0], _p(a)))
+
+
+def calculate_pso(chain, size: int, randoms: np.ndarray, inertia=0.5, local=0.5, glob=1.25, iterations=15,
+                  angle_weight=3.0, distance_weight=0.0, positions=None):
+    """One reference solve.  Advances `randoms` in place.
+    Returns (result [D], particles [3, D, size], bests [size])."""
+    c = _chain(chain)
+    D = 3 * (c.shape[0] - 1)
+    parts = np.zeros((3, D, size), dtype=np.float32)
+    bests = np.zeros(size, dtype=np.float32)
+    res = np.zeros(D, dtype=np.float32)
+    pos = None if positions is None else np.ascontiguousarray(positions, dtype=np.float32)
+    load().orc_calculate_pso(_p(parts), _p(pos), _p(bests), _p(randoms), int(size), _p(c), c.shape[0], inertia,
+                             local, glob, int(iterations), angle_weight, distance_weight, _p(res))
+    return res, parts, bests
+
+
+def solve_batch(chain, targets, start_pose, particles: int, iterations: int, rng: np.ndarray, inertia=0.5,
+                local=0.5, glob=1.25, angle_weight=3.0, distance_weight=0.0, positions=None, threads: int = 0):
+    """B independent reference solves (OpenMP over swarms).  rng: [B*P] states, advanced in place.
+    Returns (angles [B, D], fitness [B], residual [B])."""
+    c = _chain(chain)
+    D = 3 * (c.shape[0] - 1)
+    t = np.ascontiguousarray(targets, dtype=np.float32)
+    B = t.shape[0]
+    sp = None if start_pose is None else np.ascontiguousarray(start_pose, dtype=np.float32)
+    pos = None if positions is None else np.ascontiguousarray(positions, dtype=np.float32)
+    ang = np.zeros((B, D), dtype=np.float32)
+    fit = np.zeros(B, dtype=np.float32)
+    res = np.zeros(B, dtype=np.float32)
+    err = load().orc_solve_batch(_p(c), c.shape[0], _p(t), _p(sp), B, int(particles), int(iterations), inertia,
+                                 local, glob, angle_weight, distance_weight, _p(pos), _p(rng), _p(ang), _p(fit),
+                                 _p(res), int(threads))
+    if err:
+        raise RuntimeError(f"orc_solve_batch failed ({err})")
+    return ang, fit, res

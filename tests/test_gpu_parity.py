@@ -1,0 +1,286 @@
+"""HIP path (through the C ABI) vs the CPU oracle on identical seeds.
+
+Tolerances (north_star: "within a stated FP32 tolerance on final joint angles
+and residual error"):
+  * integer work -- generator seeding, draw counts, final generator states,
+    argmin/gbest bookkeeping -- is compared bit for bit;
+  * REFERENCE arithmetic (the reference's operation order, no FMA) reproduces
+    the oracle bit for bit whenever the device and host sin/cos round the same
+    way (both are fp64-evaluated); we require >= 99% of compared values to be
+    bit-identical and the rest within the FAST tolerance;
+  * FAST arithmetic (closed-form FK, FMA, 1-ulp sincos):
+      FK/fitness of one pose: |dp| <= 2e-5, |df|/f <= 1e-5
+      tier A (I <= 20): |dtheta| <= 1e-4 rad, |df|/f <= 1e-5
+      tier B (I = 200/500, chaotic): per-swarm |df|/f <= 1e-3 for >= 90% of
+      swarms and mean fitness within 0.5%.
+"""
+import numpy as np
+import pytest
+
+import ikpso
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+def rng_words(states: np.ndarray) -> np.ndarray:
+    """Significant words (d, v[5]) of oracle states, as int32 [n, 6]."""
+    w = states.view(np.int32).reshape(-1, 12)
+    return w[:, :6]
+
+
+def dev(x):
+    return torch.from_numpy(np.ascontiguousarray(x)).cuda()
+
+
+@pytest.fixture(scope="module")
+def scene_chain():
+    return ikpso.reference_scene(reset=True).origin.to_cuda()
+
+
+# ----------------------------------------------------------------- RNG init
+def test_init_generators_bitexact(oracle, device):
+    n = 5000
+    r = ikpso.rng_tensor(n)
+    assert ikpso.init_generators(r, n) == 0
+    want = oracle.init_generators(n, 0)
+    got = r.cpu().numpy()
+    assert np.array_equal(got.view(np.uint8).reshape(n, 48), want.view(np.uint8).reshape(n, 48))
+    r2 = ikpso.rng_tensor(100)
+    assert ikpso.init_generators_seeded(r2, 100, (1 << 32) + 17) == 0
+    torch.cuda.synchronize()
+    assert np.array_equal(r2.cpu().numpy()[:, :6], rng_words(oracle.init_generators(100, (1 << 32) + 17)))
+
+
+# ------------------------------------------------------------ FK + fitness
+@pytest.mark.parametrize("arith", ["fast", "reference"])
+def test_evaluate_matches_kat_and_oracle(oracle, device, fk_kat, scene_chain, arith):
+    s = ikpso.BatchSolver(scene_chain, 64, arith=arith)
+    ang = fk_kat["degrees"]
+    fit, pos = s.evaluate(dev(ang))
+    pos = pos.cpu().numpy().reshape(len(ang), 21)
+    fit = fit.cpu().numpy()
+    # the reference's own recorded positions (6 significant digits)
+    assert np.max(np.abs(pos - fk_kat["positions"])) < 1e-4
+    opos = np.array([oracle.node_positions(scene_chain, a).ravel() for a in ang])
+    ofit = np.array([oracle.fitness(scene_chain, a) for a in ang], dtype=np.float32)
+    assert np.max(np.abs(pos - opos)) < 2e-5
+    assert np.max(np.abs(fit - ofit) / np.maximum(ofit, 1e-6)) < 1e-5
+    if arith == "reference":
+        assert np.mean(pos == opos) > 0.99 and np.mean(fit == ofit) > 0.99
+    s.close()
+
+
+def test_evaluate_random_poses_and_targets(oracle, device, scene_chain):
+    rng = np.random.default_rng(1)
+    n = 2000
+    ang = rng.uniform(-7, 7, (n, 21)).astype(np.float32)
+    rest = rng.uniform(0, 6.3, (n, 21)).astype(np.float32)
+    tg = rng.uniform(-3, 3, (n, 3, 3)).astype(np.float32)
+    for arith in ("fast", "reference"):
+        s = ikpso.BatchSolver(scene_chain, 64, arith=arith)
+        fit, pos = s.evaluate(dev(ang), dev(tg), dev(rest))
+        fit = fit.cpu().numpy()
+        of = []
+        for i in range(n):
+            ch = scene_chain.copy()
+            ch["target_position"][5:8] = tg[i]
+            ch["rotation"][1:] = rest[i].reshape(7, 3)
+            of.append(oracle.fitness(ch, ang[i]))
+        of = np.array(of, dtype=np.float32)
+        assert np.max(np.abs(fit - of) / np.maximum(of, 1e-6)) < 2e-5, arith
+        s.close()
+
+
+# ------------------------------------------------------- calculatePSO parity
+def run_compat(chain, P, I, arith, seed_base=0, monkeypatch=None, positions=None, dw=0.0):
+    D = 3 * (chain.shape[0] - 1)
+    parts = ikpso.particles_tensor(P, D)
+    bests = torch.zeros(P, dtype=torch.float32, device="cuda")
+    r = ikpso.rng_tensor(P)
+    assert ikpso.init_generators_seeded(r, P, seed_base) == 0
+    res = np.zeros(D, dtype=np.float32)
+    st = ikpso.calculate_pso(parts, positions, bests, r, P, chain, ikpso.PSOConfig(0.5, 0.5, 1.25, I),
+                             ikpso.FitnessConfig(3.0, dw, 0.1), res)
+    assert st == 0
+    return res, parts.cpu().numpy(), bests.cpu().numpy(), r.cpu().numpy()
+
+
+@pytest.mark.parametrize("arith", ["fast", "reference"])
+@pytest.mark.parametrize("P", [1, 65, 256, 1024])
+def test_calculate_pso_init_is_exact(oracle, device, scene_chain, monkeypatch, arith, P):
+    """I = 0: warm start, velocity draws, pbest, argmin, result and generator states."""
+    monkeypatch.setenv("IKPSO_ARITH", arith)
+    res, parts, bests, r = run_compat(scene_chain, P, 0, arith)
+    ostate = oracle.init_generators(P, 0)
+    ores, oparts, obests = oracle.calculate_pso(scene_chain, P, ostate, iterations=0)
+    assert np.array_equal(parts, oparts)             # x = rest, v = U*2-1, pbest = x: bit-exact
+    assert np.array_equal(r[:, :6], rng_words(ostate))
+    assert np.allclose(bests, obests, rtol=1e-5, atol=0)
+    assert np.array_equal(res, ores)                 # all particles start at the rest pose
+
+
+@pytest.mark.parametrize("arith", ["fast", "reference"])
+def test_calculate_pso_one_step(oracle, device, scene_chain, monkeypatch, arith):
+    monkeypatch.setenv("IKPSO_ARITH", arith)
+    P = 1024
+    res, parts, bests, r = run_compat(scene_chain, P, 1, arith)
+    ostate = oracle.init_generators(P, 0)
+    ores, oparts, obests = oracle.calculate_pso(scene_chain, P, ostate, iterations=1)
+    assert np.array_equal(r[:, :6], rng_words(ostate))
+    if arith == "reference":
+        assert np.mean(parts == oparts) > 0.99
+    assert np.max(np.abs(parts - oparts)) < 1e-5
+    assert np.max(np.abs(bests - obests) / obests) < 1e-5
+
+
+@pytest.mark.parametrize("arith", ["fast", "reference"])
+@pytest.mark.parametrize("P,I", [(256, 20), (1024, 20)])
+def test_tier_a(oracle, device, scene_chain, monkeypatch, arith, P, I):
+    monkeypatch.setenv("IKPSO_ARITH", arith)
+    res, parts, bests, r = run_compat(scene_chain, P, I, arith)
+    ostate = oracle.init_generators(P, 0)
+    ores, oparts, obests = oracle.calculate_pso(scene_chain, P, ostate, iterations=I)
+    assert np.array_equal(r[:, :6], rng_words(ostate))  # draw count: D + 3*D*I per particle
+    assert np.max(np.abs(res - ores)) < 1e-4
+    assert abs(bests.min() - obests.min()) / obests.min() < 1e-5
+    assert np.argmin(bests) == np.argmin(obests)
+
+
+def test_tier_b_config1_and_2(oracle, device, scene_chain, monkeypatch):
+    """Chaotic regime: final fitness/residual statistically equal over several seeds."""
+    for (P, I, seeds) in ((256, 200, 8), (1024, 500, 4)):
+        gf, of_, gr, orr = [], [], [], []
+        for k in range(seeds):
+            base = k * 1_000_003
+            res, _, bests, _ = run_compat(scene_chain, P, I, "fast", seed_base=base)
+            ostate = oracle.init_generators(P, base)
+            ores, _, obests = oracle.calculate_pso(scene_chain, P, ostate, iterations=I)
+            gf.append(bests.min()), of_.append(obests.min())
+            gr.append(oracle.residual(scene_chain, res)), orr.append(oracle.residual(scene_chain, ores))
+        gf, of_ = np.array(gf), np.array(of_)
+        rel = np.abs(gf - of_) / of_
+        assert np.mean(rel <= 1e-3) >= 0.75, (P, I, rel)
+        assert abs(gf.mean() - of_.mean()) / of_.mean() < 5e-3
+        assert abs(np.mean(gr) - np.mean(orr)) < 1e-3 + 0.01 * np.mean(orr)
+
+
+def test_distance_weight_term(oracle, device, monkeypatch):
+    """distanceWeight != 0 reads positions[] at slot (k-1)*4 (src/kernel.cu:94-98)."""
+    monkeypatch.setenv("IKPSO_ARITH", "reference")
+    s = ikpso.reference_scene(reset=True)
+    chain = s.origin.to_cuda()
+    positions = s.origin.fill_positions()
+    P, I = 128, 10
+    res, parts, bests, r = run_compat(chain, P, I, "reference", positions=positions, dw=1.0)
+    ostate = oracle.init_generators(P, 0)
+    ores, oparts, obests = oracle.calculate_pso(chain, P, ostate, iterations=I, distance_weight=1.0,
+                                                positions=positions)
+    assert np.max(np.abs(res - ores)) < 1e-4
+    assert abs(bests.min() - obests.min()) / obests.min() < 1e-5
+
+
+def test_generic_tree_topology(oracle, device, monkeypatch):
+    """A non-reference tree (runtime parents, 2 effectors) through the generic kernel."""
+    o = ikpso.OriginNode((0.1, -0.2, 0.3), (0.2, 0.1, -0.3), (0, 0, 0), (6.28, 6.28, 6.28))
+    a = o.attach_child(ikpso.Node((0.3, 0.5, 0.1), (-3, -3, -3), (3, 3, 3), 0.8))
+    b = o.attach_child(ikpso.Node((0.0, 0.2, 0.7), (-3, -3, -3), (3, 3, 3), 1.1))
+    a.attach_child(ikpso.EffectorNode(2.0, (0.1, 0.1, 0.1), (-3, -3, -3), (3, 3, 3), 0.6,
+                                      ikpso.TargetNode((1.0, 0.5, 0.2))))
+    b.attach_child(ikpso.EffectorNode(0.5, (0.2, 0.0, 0.4), (-1, -1, -1), (1, 1, 1), 0.9,
+                                      ikpso.TargetNode((-0.5, 1.0, 0.8))))
+    chain = o.to_cuda()
+    assert chain["parent_index"].tolist() == [-1, 0, 1, 0, 3]
+    for arith in ("fast", "reference"):
+        monkeypatch.setenv("IKPSO_ARITH", arith)
+        res, parts, bests, r = run_compat(chain, 200, 15, arith)
+        ostate = oracle.init_generators(200, 0)
+        ores, oparts, obests = oracle.calculate_pso(chain, 200, ostate, iterations=15)
+        assert np.array_equal(r[:, :6], rng_words(ostate))
+        assert np.max(np.abs(res - ores)) < 1e-4, arith
+        assert abs(bests.min() - obests.min()) / obests.min() < 1e-5
+
+
+# ------------------------------------------------------------ batched API
+@pytest.fixture(scope="module")
+def batch_case(oracle):
+    wl = ikpso.workload(3)
+    B, P, I = 24, 1024, 20
+    tg = wl.targets(0, B)
+    ostate = oracle.init_generators(B * P, 0)
+    oang, ofit, ores = oracle.solve_batch(wl.chain, tg, None, P, I, ostate, threads=8)
+    return wl, B, P, I, tg, oang, ofit, ores
+
+
+def test_batch_vs_oracle(device, batch_case):
+    wl, B, P, I, tg, oang, ofit, ores = batch_case
+    s = ikpso.BatchSolver(wl.chain, P, pso=wl.pso)
+    s.seed(B)
+    ang, fit, res = s.solve(dev(tg), iterations=I)
+    ang, fit, res = ang.cpu().numpy(), fit.cpu().numpy(), res.cpu().numpy()
+    assert np.max(np.abs(ang - oang)) < 1e-4
+    assert np.max(np.abs(fit - ofit) / ofit) < 1e-5
+    assert np.max(np.abs(res - ores)) < 1e-4
+    s.close()
+
+
+def test_batch_sharding_invariance(device, batch_case):
+    """Per-swarm results are identical whatever the shard layout (global seeds)."""
+    wl, B, P, I, tg, *_ = batch_case
+    full = ikpso.BatchSolver(wl.chain, P, pso=wl.pso)
+    full.seed(B)
+    a_full, f_full, r_full = (t.cpu().numpy() for t in full.solve(dev(tg), iterations=I))
+    parts = []
+    for first, count in ((0, 5), (5, 11), (16, 8)):
+        s = ikpso.BatchSolver(wl.chain, P, pso=wl.pso)
+        s.seed(count, first_swarm=first)
+        parts.append([t.cpu().numpy() for t in s.solve(dev(tg[first:first + count]), iterations=I)])
+        s.close()
+    assert np.array_equal(np.concatenate([p[0] for p in parts]), a_full)
+    assert np.array_equal(np.concatenate([p[1] for p in parts]), f_full)
+    assert np.array_equal(np.concatenate([p[2] for p in parts]), r_full)
+    full.close()
+
+
+def test_batch_rng_persists_across_calls(oracle, device):
+    """Two consecutive solves continue the generator streams (like the reference's randoms)."""
+    wl = ikpso.workload(3)
+    B, P, I = 4, 256, 5
+    tg = wl.targets(0, B)
+    s = ikpso.BatchSolver(wl.chain, P, pso=wl.pso)
+    s.seed(B)
+    s.solve(dev(tg), iterations=I)
+    a2, f2, _ = (t.cpu().numpy() for t in s.solve(dev(tg), iterations=I))
+    ostate = oracle.init_generators(B * P, 0)
+    oracle.solve_batch(wl.chain, tg, None, P, I, ostate)
+    oa2, of2, _ = oracle.solve_batch(wl.chain, tg, None, P, I, ostate)
+    assert np.max(np.abs(a2 - oa2)) < 1e-4
+    assert np.max(np.abs(f2 - of2) / of2) < 1e-5
+    s.close()
+
+
+def test_batch_start_pose(oracle, device):
+    wl = ikpso.workload(3)
+    B, P, I = 6, 128, 10
+    tg = wl.targets(100, B)
+    rng = np.random.default_rng(3)
+    sp = rng.uniform(0.2, 2.0, (B, 21)).astype(np.float32)
+    s = ikpso.BatchSolver(wl.chain, P, pso=wl.pso, arith="reference")
+    s.seed(B, first_swarm=100)
+    ang, fit, res = (t.cpu().numpy() for t in s.solve(dev(tg), dev(sp), iterations=I))
+    ostate = oracle.init_generators(B * P, 100 * P)
+    oang, ofit, ores = oracle.solve_batch(wl.chain, tg, sp, P, I, ostate)
+    assert np.max(np.abs(ang - oang)) < 1e-4
+    assert np.max(np.abs(fit - ofit) / ofit) < 1e-5
+    s.close()
+
+
+def test_empty_and_invalid(device, scene_chain):
+    s = ikpso.BatchSolver(scene_chain, 64)
+    s.seed(2)
+    a, f, r = s.solve(torch.zeros((0, 3, 3), device="cuda"), iterations=3)
+    assert a.shape == (0, 21)
+    with pytest.raises(ikpso.IkpsoError):
+        s.solve(torch.zeros((3, 3, 3), device="cuda"), iterations=3)  # beyond seeded capacity
+    s.close()
