@@ -67,6 +67,10 @@ M4 m4_mul(const M4& l, const M4& r)
     return o;
 }
 
+// Correctly rounded fp32 sin/cos: what the device REFERENCE mode computes.
+float sin_cr(float x) { return (float)sin((double)x); }
+float cos_cr(float x) { return (float)cos((double)x); }
+
 M4 origin_matrix(const ikpso_node& n)
 {
     M4 m = m4_create(1.0f);
@@ -77,22 +81,22 @@ M4 origin_matrix(const ikpso_node& n)
     m = m4_mul(m, t);
     const float a = n.rotation[0], b = n.rotation[1], c = n.rotation[2];
     M4 rx = m4_create(1.0f);
-    rx.c[5] = cosf(a);
-    rx.c[6] = -sinf(a);
-    rx.c[9] = sinf(a);
-    rx.c[10] = cosf(a);
+    rx.c[5] = cos_cr(a);
+    rx.c[6] = -sin_cr(a);
+    rx.c[9] = sin_cr(a);
+    rx.c[10] = cos_cr(a);
     m = m4_mul(m, rx);
     M4 ry = m4_create(1.0f);
-    ry.c[0] = cosf(b);
-    ry.c[2] = sinf(b);
-    ry.c[8] = -sinf(b);
-    ry.c[10] = cosf(b);
+    ry.c[0] = cos_cr(b);
+    ry.c[2] = sin_cr(b);
+    ry.c[8] = -sin_cr(b);
+    ry.c[10] = cos_cr(b);
     m = m4_mul(m, ry);
     M4 rz = m4_create(1.0f);
-    rz.c[0] = cosf(c);
-    rz.c[1] = -sinf(c);
-    rz.c[4] = sinf(c);
-    rz.c[5] = cosf(c);
+    rz.c[0] = cos_cr(c);
+    rz.c[1] = -sin_cr(c);
+    rz.c[4] = sin_cr(c);
+    rz.c[5] = cos_cr(c);
     return m4_mul(m, rz);
 }
 
@@ -201,6 +205,7 @@ ikpso_status scratch(size_t bytes, float** out)
 
 struct ikpso_solver {
     ChainHost chain;
+    float* aux = nullptr;  // device copy of chain.aux
     int P = 0;
     int mode = IKPSO_ARITH_FAST;
     ikpso_rng_state* rng = nullptr;
@@ -268,10 +273,14 @@ ikpso_status ikpso_calculate_pso(float* particles, const float* positions, float
     if (st != IKPSO_OK) return st;
     if (size > resident_max_threads(ch)) return IKPSO_ERR_UNSUPPORTED;  // streaming kernels: next
 
+    // device scratch: [result D | aux 10J]; aux (positions term) is uploaded
+    // here and the call synchronises before returning, so `ch.aux` outlives it
     float* dres = nullptr;
-    st = scratch(sizeof(float) * D, &dres);
+    st = scratch(sizeof(float) * (D + ch.aux.size()), &dres);
     if (st != IKPSO_OK) return st;
     const hipStream_t s = (hipStream_t)stream;
+    IKPSO_HIP(hipMemcpyAsync(dres + D, ch.aux.data(), sizeof(float) * ch.aux.size(), hipMemcpyHostToDevice, s));
+    ch.aux_dev = dres + D;
     SwarmIO io{};
     io.targets = nullptr;
     io.start_pose = nullptr;
@@ -331,7 +340,19 @@ ikpso_status ikpso_solver_create(const ikpso_solver_desc* desc, ikpso_solver** o
     }
     s->P = desc->particles;
     s->mode = desc->arith;
+    {
+        const size_t bytes = sizeof(float) * s->chain.aux.size();
+        hipError_t e = hipMalloc(&s->aux, bytes);
+        if (e == hipSuccess) e = hipMemcpy(s->aux, s->chain.aux.data(), bytes, hipMemcpyHostToDevice);
+        if (e != hipSuccess) {
+            if (s->aux) (void)hipFree(s->aux);
+            delete s;
+            return hip_status(e);
+        }
+        s->chain.aux_dev = s->aux;
+    }
     if (s->P > resident_max_threads(s->chain)) {  // streaming kernels: next
+        (void)hipFree(s->aux);
         delete s;
         return IKPSO_ERR_UNSUPPORTED;
     }
@@ -343,6 +364,7 @@ ikpso_status ikpso_solver_destroy(ikpso_solver* s)
 {
     if (!s) return IKPSO_OK;
     if (s->rng) (void)hipFree(s->rng);
+    if (s->aux) (void)hipFree(s->aux);
     delete s;
     return IKPSO_OK;
 }

@@ -67,7 +67,7 @@ __device__ __attribute__((noinline)) void sincos_slow(float x, float* s, float* 
 // FAST: Cody-Waite reduction by pi/2 with three FMA steps, then minimax
 // polynomials on [-pi/4, pi/4] (sin: odd degree 7, cos: even degree 8; about
 // 1 ulp).
-__device__ __forceinline__ void sincos_fast(float x, float* s_out, float* c_out)
+__host__ __device__ __forceinline__ void sincos_fast(float x, float* s_out, float* c_out)
 {
     const float k = __builtin_rintf(x * 0.636619772367581343f);
     float r = __builtin_fmaf(-k, 1.57079637050628662109375f, x);
@@ -94,7 +94,7 @@ __device__ __forceinline__ void sincos_fast(float x, float* s_out, float* c_out)
 // the correctly rounded sinf/cosf except in vanishingly rare near-tie cases --
 // the same property the host libm's double-evaluated sinf/cosf has, which
 // keeps this mode in bitwise agreement with the CPU oracle.
-__device__ __forceinline__ void sincos_reference(float x, float* s_out, float* c_out)
+__host__ __device__ __forceinline__ void sincos_reference(float x, float* s_out, float* c_out)
 {
     const float kf = __builtin_rintf(x * 0.636619772367581343f);
     const double k = (double)kf;

@@ -350,6 +350,7 @@ const char* kernel_name(const ChainHost& ch)
 hipError_t launch_resident(const ChainHost& ch, int mode, const SwarmIO& io, hipStream_t stream)
 {
     if (io.num_swarms <= 0) return hipSuccess;
+    if (!ch.aux_dev) return hipErrorInvalidValue;  // the kernels read aux for the optional terms
     const int block = ((io.P + 63) / 64) * 64;
     hipError_t err = hipErrorInvalidValue;
     const bool ok = visit_topology(ch, [&](auto topo) {
@@ -365,6 +366,7 @@ hipError_t launch_resident(const ChainHost& ch, int mode, const SwarmIO& io, hip
 hipError_t launch_evaluate(const ChainHost& ch, int mode, const EvalIO& io, hipStream_t stream)
 {
     if (io.n <= 0) return hipSuccess;
+    if (!ch.aux_dev) return hipErrorInvalidValue;
     hipError_t err = hipErrorInvalidValue;
     const bool ok = visit_topology(ch, [&](auto topo) {
         using T = decltype(topo);

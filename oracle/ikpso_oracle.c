@@ -30,7 +30,11 @@
  * thrust::min_element (first minimum, operator<).
  *
  * Arithmetic: plain IEEE fp32, evaluated in the reference's operation order,
- * compiled with -ffp-contract=off (no FMA), libm sinf/cosf.  The three
+ * compiled with -ffp-contract=off (no FMA).  sinf/cosf: the reference calls
+ * CUDA's precise sinf/cosf (<= 2 ulp, src/matrix_operations.cuh:136-161; not
+ * available here); they are restated as the correctly rounded values
+ * (float)sin((double)x), which glibc's own sinf/cosf miss by 1 ulp on ~1.4% of
+ * arguments in [-7, 7].  The three
  * curand_uniform() calls in one expression (src/kernel.cu:164-166) are drawn
  * left to right (r1, r2, r3).
  */
@@ -73,6 +77,10 @@ typedef struct {
 enum { ORC_ORIGIN = 0, ORC_EFFECTOR = 1, ORC_NODE = 2 };
 
 typedef struct { float c[16]; } mat4; /* row-major, cells[col + 4*row] */
+
+/* correctly rounded fp32 sin/cos (see header) */
+static inline float sin_cr(float x) { return (float)sin((double)x); }
+static inline float cos_cr(float x) { return (float)cos((double)x); }
 
 int orc_sizeof_rng(void) { return (int)sizeof(orc_rng); }
 int orc_sizeof_node(void) { return (int)sizeof(orc_node); }
@@ -164,30 +172,30 @@ static mat4 m_translate(mat4 l, float x, float y, float z)
 static mat4 m_rot_x(mat4 l, float a)
 {
     mat4 m = m_create(1.0f);
-    m.c[5] = cosf(a);
-    m.c[6] = -sinf(a);
-    m.c[9] = sinf(a);
-    m.c[10] = cosf(a);
+    m.c[5] = cos_cr(a);
+    m.c[6] = -sin_cr(a);
+    m.c[9] = sin_cr(a);
+    m.c[10] = cos_cr(a);
     return m_mul(l, m);
 }
 
 static mat4 m_rot_y(mat4 l, float a)
 {
     mat4 m = m_create(1.0f);
-    m.c[0] = cosf(a);
-    m.c[2] = sinf(a);
-    m.c[8] = -sinf(a);
-    m.c[10] = cosf(a);
+    m.c[0] = cos_cr(a);
+    m.c[2] = sin_cr(a);
+    m.c[8] = -sin_cr(a);
+    m.c[10] = cos_cr(a);
     return m_mul(l, m);
 }
 
 static mat4 m_rot_z(mat4 l, float a)
 {
     mat4 m = m_create(1.0f);
-    m.c[0] = cosf(a);
-    m.c[1] = -sinf(a);
-    m.c[4] = sinf(a);
-    m.c[5] = cosf(a);
+    m.c[0] = cos_cr(a);
+    m.c[1] = -sin_cr(a);
+    m.c[4] = sin_cr(a);
+    m.c[5] = cos_cr(a);
     return m_mul(l, m);
 }
 
