@@ -190,7 +190,7 @@ def main():
             "peak": valu["peak"] if valu else HBM_PEAK_GBS,
             "unit": valu["unit"] if valu else "GB/s",
             "frac": valu["frac"] if valu else round(alg_gbs / HBM_PEAK_GBS, 4),
-            "traffic": vpu.get("hbm_bytes_per_launch") if vpu else None,
+            "traffic": round(vpu["hbm_bytes_per_update"] * ups_launch) if vpu else None,
             "kernel": "k_swarm_resident<TopoRef7,FAST> (one launch = one batch)",
             "kernel_ms": round(kern_ms, 3),
             "hbm_algorithmic": {

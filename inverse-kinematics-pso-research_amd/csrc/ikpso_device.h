@@ -15,6 +15,13 @@
 
 #include "ikpso_params.h"
 
+#ifndef IKPSO_SCHED_NODE
+#define IKPSO_SCHED_NODE 0
+#endif
+#ifndef IKPSO_SCHED_DIM
+#define IKPSO_SCHED_DIM 0
+#endif
+
 namespace ikpso {
 
 // ---------------------------------------------------------------- XORWOW
@@ -22,7 +29,7 @@ namespace ikpso {
 struct Xorwow {
     uint32_t d, v0, v1, v2, v3, v4;
 
-    __device__ __forceinline__ uint32_t next()
+    __host__ __device__ __forceinline__ uint32_t next()
     {
         const uint32_t t = v0 ^ (v0 >> 2);
         v0 = v1;
@@ -35,9 +42,14 @@ struct Xorwow {
     }
     // x * 2^-32 + 2^-33 in (0, 1]; the product is exact, so fused or not the
     // result is the same single rounding.
-    __device__ __forceinline__ float uniform()
+    __host__ __device__ __forceinline__ float uniform()
     {
+#if IKPSO_ABL_NORNG  // timing-only ablation: no state advance
+        v4 += 0x9e3779b9u;
+        return __builtin_fmaf((float)v4, 2.3283064e-10f, 1.16415322e-10f);
+#else
         return __builtin_fmaf((float)next(), 2.3283064e-10f, 1.16415322e-10f);
+#endif
     }
 };
 
@@ -69,6 +81,11 @@ __device__ __attribute__((noinline)) void sincos_slow(float x, float* s, float* 
 // 1 ulp).
 __host__ __device__ __forceinline__ void sincos_fast(float x, float* s_out, float* c_out)
 {
+#if IKPSO_ABL_NOSIN  // timing-only ablation
+    *s_out = x * 0.5f;
+    *c_out = __builtin_fmaf(-0.5f, x, 1.0f);
+    return;
+#endif
     const float k = __builtin_rintf(x * 0.636619772367581343f);
     float r = __builtin_fmaf(-k, 1.57079637050628662109375f, x);
     r = __builtin_fmaf(-k, -4.37113900018624283e-8f, r);
@@ -304,9 +321,11 @@ __device__ __forceinline__ float fitness(const ChainConsts<Topo::J>& cc, const f
             node_pos[3 * (k - 1) + 1] = F[k].py;
             node_pos[3 * (k - 1) + 2] = F[k].pz;
         }
-        // One node at a time: without this the scheduler hoists all 3J
-        // independent sincos evaluations to the top and spills the state.
+#if IKPSO_SCHED_NODE
+        // One node at a time: keeps the scheduler from hoisting all 3J
+        // independent sincos evaluations to the top of the evaluation.
         __builtin_amdgcn_sched_barrier(0);
+#endif
     }
     float f = posref ? (distance + cc.dw_j * pos_diff) + cc.aw_j * rot_diff : distance + cc.aw_j * rot_diff;
     if (cc.use_penalty) {  // soft joint-limit penalty (extension, BASELINE config 5)

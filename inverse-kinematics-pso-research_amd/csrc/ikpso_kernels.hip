@@ -182,7 +182,9 @@ __global__ void __launch_bounds__(kResidentMaxThreads<Topo::J>())
 #pragma unroll
         for (int d = 0; d < D; ++d) {
             pso_update<MODE>(x[d], v[d], s_pb[d * BLOCK + tid], sh.g[d], w, c1, c2, rng);
+#if IKPSO_SCHED_DIM
             if (d % 3 == 2) __builtin_amdgcn_sched_barrier(0);
+#endif
         }
 #pragma unroll
         for (int d = 0; d < D; ++d) x[d] = clamp_ref(x[d], sh.lo[d], sh.hi[d]);
@@ -196,7 +198,12 @@ __global__ void __launch_bounds__(kResidentMaxThreads<Topo::J>())
         }
 
         // thrust::min_element + `globalMin > currentGlobalMin` (src/kernel.cu:315-323)
+#if IKPSO_ABL_NOSYNC  // timing-only ablation: no swarm argmin
+        const uint32_t bmin = gkey;
+        asm volatile("" ::"v"(pbf));
+#else
         const uint32_t bmin = swarm_argmin<J>(sh, (it + 1) & 1, active ? ordered_key(pbf) : 0xFFFFFFFFu, &bidx);
+#endif
         if (bmin < gkey) {  // uniform across the workgroup
             gkey = bmin;
             if (tid < D) sh.g[tid] = s_pb[tid * BLOCK + bidx];

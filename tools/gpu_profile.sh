@@ -1,0 +1,20 @@
+#!/bin/bash
+# rocprofv3 kernel trace + PMC passes (one counter group per pass; no tracing
+# domains combined with --pmc) for the bench workload.  Outputs in gpurun_out/prof_*.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+ARGS=${PROF_ARGS:-"--swarms-per-gpu 2048 --steps 2 --warmup 1 --cpu-seconds 0"}
+run() {  # run NAME ROCPROF_ARGS...
+  local name=$1; shift
+  echo "== $name"
+  timeout -k 10 600 rocprofv3 "$@" -d "gpurun_out/prof_$name" -o run --output-format csv -- python3 bench.py $ARGS \
+    > "gpurun_out/prof_$name.log" 2>&1
+  local rc=$?; echo "   rc=$rc"; [ $rc -eq 0 ] || { tail -20 "gpurun_out/prof_$name.log"; exit $rc; }
+}
+run trace --kernel-trace --stats
+run valu --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVES GRBM_GUI_ACTIVE
+run fetch --pmc FETCH_SIZE
+run write --pmc WRITE_SIZE
+run cycles --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY
+echo ALL_DONE

@@ -1,0 +1,78 @@
+#!/usr/bin/env python3
+"""Time several builds of libikpso.so on the bench workload, interleaved in ONE
+process (rounds x variants), so clock/DVFS drift hits every variant alike.
+usage: variant_bench.py LIB [LIB...] [--swarms N] [--rounds R] [--iters I]"""
+import argparse
+import ctypes
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT / "inverse-kinematics-pso-research_amd"))
+
+import numpy as np
+import torch
+
+import ikpso
+from ikpso import _abi
+
+
+def open_lib(path):
+    lib = ctypes.CDLL(str(path))
+    for name, (res, args) in _abi.SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype, fn.argtypes = res, args
+    return lib
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("libs", nargs="+")
+    ap.add_argument("--swarms", type=int, default=4096)
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--iters", type=int, default=500)
+    ap.add_argument("--arith", default="fast")
+    a = ap.parse_args()
+    wl = ikpso.workload(3)
+    P, I, B = 1024, a.iters, a.swarms
+    tg = torch.from_numpy(wl.targets(0, B)).cuda()
+    outs = [torch.empty((B, 21), device="cuda"), torch.empty(B, device="cuda"), torch.empty(B, device="cuda")]
+    solvers = []
+    for p in a.libs:
+        lib = open_lib(p)
+        desc = _abi.SolverDesc()
+        chain = np.ascontiguousarray(wl.chain)
+        desc.chain = chain.ctypes.data
+        desc.node_count = 8
+        desc.particles = P
+        desc.pso = _abi.PSOConfig(0.5, 0.5, 1.25, I)
+        desc.fit = _abi.FitnessConfig(3.0, 0.0, 0.1)
+        desc.arith = 0 if a.arith == "fast" else 1
+        h = ctypes.c_void_p()
+        assert lib.ikpso_solver_create(ctypes.byref(desc), ctypes.byref(h)) == 0
+        assert lib.ikpso_solver_seed(h, B, 0, 0, None) == 0
+        solvers.append((p, lib, h, chain))
+    times = {p: [] for p in a.libs}
+    results = {}
+    for r in range(a.rounds + 1):
+        for p, lib, h, _ in solvers:
+            assert lib.ikpso_solver_seed(h, B, 0, 0, None) == 0
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            assert lib.ikpso_solve_batch(h, tg.data_ptr(), None, B, I, outs[0].data_ptr(), outs[1].data_ptr(),
+                                         outs[2].data_ptr(), None) == 0
+            e1.record()
+            torch.cuda.synchronize()
+            if r:
+                times[p].append(e0.elapsed_time(e1))
+            results[p] = float(outs[1].mean())
+    for p in a.libs:
+        t = np.array(times[p])
+        ups = B * P * I / (np.median(t) / 1e3)
+        print(f"{Path(p).name:40s} median {np.median(t):8.3f} ms  min {t.min():8.3f}  "
+              f"{ups:.3e} upd/s  mean_fit {results[p]:.6f}")
+
+
+if __name__ == "__main__":
+    main()
