@@ -91,6 +91,13 @@ typedef struct ikpso_collider {
     float quat[4]; /* float4, 16-byte aligned in the reference */
 } ikpso_collider;
 
+/* Kernel family (ikpso_solver_desc.kernel; env IKPSO_KERNEL for ikpso_calculate_pso). */
+enum {
+    IKPSO_KERNEL_AUTO = 0,      /* resident when the swarm fits one workgroup, else streaming */
+    IKPSO_KERNEL_RESIDENT = 1,  /* one workgroup per swarm, state on chip, one launch per batch */
+    IKPSO_KERNEL_STREAMING = 2  /* state in HBM, one launch per iteration, any swarm size */
+};
+
 /* Arithmetic mode of the device kernels. */
 enum {
     IKPSO_ARITH_FAST = 0,      /* closed-form 3x3 FK, FMA contraction (default) */
@@ -138,7 +145,7 @@ typedef struct ikpso_solver_desc {
     ikpso_pso_config pso;
     ikpso_fitness_config fit;
     int32_t arith;            /* IKPSO_ARITH_* */
-    int32_t reserved0;
+    int32_t kernel;           /* IKPSO_KERNEL_* */
     const float* positions;   /* any, [4*J] or NULL (distance term, as calculatePSO) */
     /* Optional soft joint-limit penalty (a new term; the reference only clamps):
      * fitness += limit_weight * sum_d max(0, x_d - soft_hi[d], soft_lo[d] - x_d)^2 */
@@ -180,7 +187,7 @@ ikpso_status ikpso_solver_evaluate(ikpso_solver* solver, const float* angles, co
 /* Introspection. */
 int ikpso_solver_dof(const ikpso_solver* solver);
 int ikpso_solver_effectors(const ikpso_solver* solver);
-/* Name of the kernel variant the solver dispatches to (topology / residency). */
+/* Name of the kernel variant the solver dispatches to (family / topology). */
 const char* ikpso_solver_kernel_name(const ikpso_solver* solver);
 
 int ikpso_abi_version(void);

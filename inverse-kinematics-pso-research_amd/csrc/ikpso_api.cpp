@@ -182,14 +182,14 @@ ikpso_status parse_chain(const std::vector<ikpso_node>& nodes, const ikpso_pso_c
     return IKPSO_OK;
 }
 
-// Small device scratch for the reference-compatible path (result staging).
+// Device scratch of the reference-compatible path (result staging, aux terms,
+// streaming workspace).  The entry point holds g_scratch_mu for its whole call.
 std::mutex g_scratch_mu;
 float* g_scratch = nullptr;
 size_t g_scratch_bytes = 0;
 
 ikpso_status scratch(size_t bytes, float** out)
 {
-    std::lock_guard<std::mutex> lk(g_scratch_mu);
     if (g_scratch_bytes < bytes) {
         if (g_scratch) (void)hipFree(g_scratch);
         g_scratch = nullptr;
@@ -201,11 +201,68 @@ ikpso_status scratch(size_t bytes, float** out)
     return IKPSO_OK;
 }
 
+// Carve 256-byte aligned arrays out of one allocation.
+struct Carver {
+    char* base;
+    size_t off = 0;
+    template <class T>
+    T* take(size_t n)
+    {
+        off = (off + 255) & ~size_t(255);
+        T* p = reinterpret_cast<T*>(base + off);
+        off += n * sizeof(T);
+        return p;
+    }
+};
+
+// Streaming workspace layout (see StreamIO); state/pbf carved only when not
+// supplied by the caller.
+void carve_stream(StreamIO& io, void* ws, int64_t B, int P, int D, bool own_state)
+{
+    Carver cv{static_cast<char*>(ws)};
+    const int C = (P + kStreamChunk - 1) / kStreamChunk;
+    if (own_state) {
+        io.state = cv.take<float>((size_t)B * 3 * D * P);
+        io.pbf = cv.take<float>((size_t)B * P);
+    }
+    io.rng = cv.take<uint32_t>((size_t)6 * B * P);
+    io.pkey = cv.take<uint32_t>((size_t)2 * B * C);
+    io.pidx = cv.take<int32_t>((size_t)2 * B * C);
+    io.pvec = cv.take<float>((size_t)2 * B * C * D);
+    io.gkey = cv.take<uint32_t>((size_t)2 * B);
+    io.gidx = cv.take<int32_t>((size_t)2 * B);
+    io.gvec = cv.take<float>((size_t)2 * B * D);
+    io.num_swarms = B;
+    io.P = P;
+    io.C = C;
+}
+
+int env_kernel()
+{
+    const char* e = getenv("IKPSO_KERNEL");
+    if (!e) return IKPSO_KERNEL_AUTO;
+    if (strcmp(e, "resident") == 0) return IKPSO_KERNEL_RESIDENT;
+    if (strcmp(e, "streaming") == 0) return IKPSO_KERNEL_STREAMING;
+    return IKPSO_KERNEL_AUTO;
+}
+
+// Resolve the kernel family for a chain and swarm size; -1 if impossible.
+int pick_kernel(const ChainHost& ch, int P, int requested)
+{
+    const bool fits = P <= resident_max_threads(ch);
+    if (requested == IKPSO_KERNEL_RESIDENT) return fits ? IKPSO_KERNEL_RESIDENT : -1;
+    if (requested == IKPSO_KERNEL_STREAMING) return IKPSO_KERNEL_STREAMING;
+    return fits ? IKPSO_KERNEL_RESIDENT : IKPSO_KERNEL_STREAMING;
+}
+
 }  // namespace
 
 struct ikpso_solver {
     ChainHost chain;
     float* aux = nullptr;  // device copy of chain.aux
+    int family = IKPSO_KERNEL_RESIDENT;
+    void* ws = nullptr;    // streaming workspace
+    size_t ws_bytes = 0;
     int P = 0;
     int mode = IKPSO_ARITH_FAST;
     ikpso_rng_state* rng = nullptr;
@@ -271,33 +328,44 @@ ikpso_status ikpso_calculate_pso(float* particles, const float* positions, float
     ChainHost ch;
     st = parse_chain(nodes, pso, fit, ex, ch);
     if (st != IKPSO_OK) return st;
-    if (size > resident_max_threads(ch)) return IKPSO_ERR_UNSUPPORTED;  // streaming kernels: next
-
-    // device scratch: [result D | aux 10J]; aux (positions term) is uploaded
-    // here and the call synchronises before returning, so `ch.aux` outlives it
-    float* dres = nullptr;
-    st = scratch(sizeof(float) * (D + ch.aux.size()), &dres);
-    if (st != IKPSO_OK) return st;
-    const hipStream_t s = (hipStream_t)stream;
-    IKPSO_HIP(hipMemcpyAsync(dres + D, ch.aux.data(), sizeof(float) * ch.aux.size(), hipMemcpyHostToDevice, s));
-    ch.aux_dev = dres + D;
-    SwarmIO io{};
-    io.targets = nullptr;
-    io.start_pose = nullptr;
-    io.rng = randoms;
-    io.out_angles = dres;
-    io.out_fitness = nullptr;
-    io.out_residual = nullptr;
-    io.dump_particles = particles;
-    io.dump_bests = bests;
-    io.P = size;
-    io.iterations = pso.iterations;
-    io.num_swarms = 1;
+    const int family = pick_kernel(ch, size, env_kernel());
+    if (family < 0) return IKPSO_ERR_UNSUPPORTED;
     // The reference-compatible entry has no mode argument; IKPSO_ARITH=reference
     // selects the reference's operation order (parity runs).
     const char* env = getenv("IKPSO_ARITH");
     const int mode = (env && strcmp(env, "reference") == 0) ? IKPSO_ARITH_REFERENCE : IKPSO_ARITH_FAST;
-    IKPSO_HIP(launch_resident(ch, mode, io, s));
+
+    std::lock_guard<std::mutex> lk(g_scratch_mu);
+    // device scratch: [result D | aux 10J | streaming workspace]; aux is
+    // uploaded here and the call synchronises before returning, so `ch.aux`
+    // outlives every use
+    const size_t head = sizeof(float) * (D + ch.aux.size());
+    const size_t ws = family == IKPSO_KERNEL_STREAMING ? stream_workspace_bytes(1, size, D, false) : 0;
+    float* dres = nullptr;
+    st = scratch(((head + 255) & ~size_t(255)) + ws, &dres);
+    if (st != IKPSO_OK) return st;
+    const hipStream_t s = (hipStream_t)stream;
+    IKPSO_HIP(hipMemcpyAsync(dres + D, ch.aux.data(), sizeof(float) * ch.aux.size(), hipMemcpyHostToDevice, s));
+    ch.aux_dev = dres + D;
+    if (family == IKPSO_KERNEL_RESIDENT) {
+        SwarmIO io{};
+        io.rng = randoms;
+        io.out_angles = dres;
+        io.dump_particles = particles;
+        io.dump_bests = bests;
+        io.P = size;
+        io.iterations = pso.iterations;
+        io.num_swarms = 1;
+        IKPSO_HIP(launch_resident(ch, mode, io, s));
+    } else {
+        StreamIO io{};
+        carve_stream(io, reinterpret_cast<char*>(dres) + ((head + 255) & ~size_t(255)), 1, size, D, false);
+        io.state = particles;  // the reference's own [3][D][P] layout is the streaming state
+        io.pbf = bests;
+        io.rng_aos = randoms;
+        io.out_angles = dres;
+        IKPSO_HIP(launch_stream(ch, mode, io, pso.iterations, s));
+    }
     IKPSO_HIP(hipMemcpyAsync(result, dres, sizeof(float) * D, hipMemcpyDefault, s));
     IKPSO_HIP(hipStreamSynchronize(s));
     return IKPSO_OK;
@@ -351,10 +419,11 @@ ikpso_status ikpso_solver_create(const ikpso_solver_desc* desc, ikpso_solver** o
         }
         s->chain.aux_dev = s->aux;
     }
-    if (s->P > resident_max_threads(s->chain)) {  // streaming kernels: next
+    s->family = pick_kernel(s->chain, s->P, desc->kernel);
+    if (s->family < 0 || desc->kernel < IKPSO_KERNEL_AUTO || desc->kernel > IKPSO_KERNEL_STREAMING) {
         (void)hipFree(s->aux);
         delete s;
-        return IKPSO_ERR_UNSUPPORTED;
+        return desc->kernel == IKPSO_KERNEL_RESIDENT ? IKPSO_ERR_UNSUPPORTED : IKPSO_ERR_INVALID_ARG;
     }
     *out = s;
     return IKPSO_OK;
@@ -365,6 +434,7 @@ ikpso_status ikpso_solver_destroy(ikpso_solver* s)
     if (!s) return IKPSO_OK;
     if (s->rng) (void)hipFree(s->rng);
     if (s->aux) (void)hipFree(s->aux);
+    if (s->ws) (void)hipFree(s->ws);
     delete s;
     return IKPSO_OK;
 }
@@ -394,19 +464,39 @@ ikpso_status ikpso_solve_batch(ikpso_solver* s, const float* targets, const floa
     if (!out_angles) return IKPSO_ERR_INVALID_ARG;  // targets == NULL: chain targets for every swarm
     if (num_swarms > s->capacity || !s->rng) return IKPSO_ERR_INVALID_ARG;  // seed first
     if (num_swarms > 0x7fffffff) return IKPSO_ERR_INVALID_ARG;
-    SwarmIO io{};
+    const hipStream_t hs = (hipStream_t)stream;
+    if (s->family == IKPSO_KERNEL_RESIDENT) {
+        SwarmIO io{};
+        io.targets = targets;
+        io.start_pose = start_pose;
+        io.rng = s->rng;
+        io.out_angles = out_angles;
+        io.out_fitness = out_fitness;
+        io.out_residual = out_residual;
+        io.P = s->P;
+        io.iterations = iterations;
+        io.num_swarms = num_swarms;
+        IKPSO_HIP(launch_resident(s->chain, s->mode, io, hs));
+        return IKPSO_OK;
+    }
+    const int D = 3 * s->chain.J;
+    const size_t need = stream_workspace_bytes(num_swarms, s->P, D, true);
+    if (need > s->ws_bytes) {
+        if (s->ws) IKPSO_HIP(hipFree(s->ws));  // hipFree synchronises the device
+        s->ws = nullptr;
+        s->ws_bytes = 0;
+        IKPSO_HIP(hipMalloc(&s->ws, need));
+        s->ws_bytes = need;
+    }
+    StreamIO io{};
+    carve_stream(io, s->ws, num_swarms, s->P, D, true);
+    io.rng_aos = s->rng;
     io.targets = targets;
     io.start_pose = start_pose;
-    io.rng = s->rng;
     io.out_angles = out_angles;
     io.out_fitness = out_fitness;
     io.out_residual = out_residual;
-    io.dump_particles = nullptr;
-    io.dump_bests = nullptr;
-    io.P = s->P;
-    io.iterations = iterations;
-    io.num_swarms = num_swarms;
-    IKPSO_HIP(launch_resident(s->chain, s->mode, io, (hipStream_t)stream));
+    IKPSO_HIP(launch_stream(s->chain, s->mode, io, iterations, hs));
     return IKPSO_OK;
 }
 
@@ -421,6 +511,9 @@ ikpso_status ikpso_solver_evaluate(ikpso_solver* s, const float* angles, const f
 
 int ikpso_solver_dof(const ikpso_solver* s) { return s ? 3 * s->chain.J : 0; }
 int ikpso_solver_effectors(const ikpso_solver* s) { return s ? s->chain.E : 0; }
-const char* ikpso_solver_kernel_name(const ikpso_solver* s) { return s ? kernel_name(s->chain) : ""; }
+const char* ikpso_solver_kernel_name(const ikpso_solver* s)
+{
+    return s ? kernel_name(s->chain, s->family == IKPSO_KERNEL_STREAMING) : "";
+}
 
 }  // extern "C"

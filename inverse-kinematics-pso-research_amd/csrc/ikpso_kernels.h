@@ -83,9 +83,11 @@ ChainConsts<J> make_consts(const ChainHost& h)
 
 hipError_t launch_init_generators(ikpso_rng_state* st, int64_t count, uint64_t seed_base, hipStream_t stream);
 hipError_t launch_resident(const ChainHost& ch, int mode, const SwarmIO& io, hipStream_t stream);
+hipError_t launch_stream(const ChainHost& ch, int mode, const StreamIO& io, int iterations, hipStream_t stream);
+size_t stream_workspace_bytes(int64_t B, int P, int D, bool with_state);
 hipError_t launch_evaluate(const ChainHost& ch, int mode, const EvalIO& io, hipStream_t stream);
 int resident_max_threads(const ChainHost& ch);
 bool chain_supported(const ChainHost& ch);
-const char* kernel_name(const ChainHost& ch);
+const char* kernel_name(const ChainHost& ch, bool streaming);
 
 }  // namespace ikpso

@@ -22,6 +22,7 @@
 
 #include "ikpso_device.h"
 #include "ikpso_kernels.h"
+#include "ikpso_swarm.h"
 
 namespace ikpso {
 
@@ -60,81 +61,6 @@ hipError_t launch_init_generators(ikpso_rng_state* st, int64_t count, uint64_t s
 }
 
 // ------------------------------------------------------- resident swarm kernel
-__device__ __forceinline__ void load_rng(Xorwow& r, const ikpso_rng_state* p)
-{
-    const uint32_t* q = reinterpret_cast<const uint32_t*>(p);
-    r.d = q[0];
-    r.v0 = q[1];
-    r.v1 = q[2];
-    r.v2 = q[3];
-    r.v3 = q[4];
-    r.v4 = q[5];
-}
-
-__device__ __forceinline__ void store_rng(const Xorwow& r, ikpso_rng_state* p)
-{
-    uint32_t* q = reinterpret_cast<uint32_t*>(p);
-    q[0] = r.d;
-    q[1] = r.v0;
-    q[2] = r.v1;
-    q[3] = r.v2;
-    q[4] = r.v3;
-    q[5] = r.v4;
-}
-
-// Per-swarm uniform constants staged in LDS.  They are read at their point of
-// use every iteration (an empty asm with a memory clobber at the top of the
-// iteration stops the compiler from hoisting them into registers): ~100
-// loop-invariant uniforms held in SGPRs/VGPRs across the loop spill, while a
-// broadcast ds_read costs one LDS cycle.
-template <int J>
-struct SwarmShared {
-    float lo[3 * J], hi[3 * J];  // clamp bounds
-    float rest[3 * J];           // warm start + angle-term reference
-    float tgt[3 * J];            // effector targets per node (k-1), 0 elsewhere
-    float g[3 * J];              // global-best vector
-    uint32_t key[2][16];         // per-wave argmin, double-buffered by parity
-    int32_t idx[2][16];
-};
-
-template <int J>
-__device__ __forceinline__ void stage_swarm_inputs(const ChainConsts<J>& cc, const SwarmIO& io, int64_t b,
-                                                   SwarmShared<J>& sh)
-{
-    constexpr int D = 3 * J;
-    const float* t = io.targets ? io.targets + b * (int64_t)cc.num_eff * 3 : nullptr;
-    for (int d = threadIdx.x; d < D; d += blockDim.x) {
-        sh.lo[d] = cc.lo[d];
-        sh.hi[d] = cc.hi[d];
-        sh.rest[d] = io.start_pose ? io.start_pose[b * D + d] : cc.rest[d];
-        const int s = cc.eff_slot[d / 3 + 1];
-        sh.tgt[d] = t ? (s >= 0 ? t[3 * s + d % 3] : 0.0f) : cc.tgt0[d];
-    }
-}
-
-__device__ __forceinline__ void compiler_fence() { asm volatile("" ::: "memory"); }
-
-// Swarm argmin of the local-best fitness keys, lowest particle index on ties
-// (thrust::min_element, src/kernel.cu:297,315).  One DPP wave min + ballot per
-// wave, a 16-entry LDS exchange, then every wave reduces the 16 entries
-// redundantly, so the result is uniform without a second barrier.
-template <int J>
-__device__ __forceinline__ uint32_t swarm_argmin(SwarmShared<J>& sh, int par, uint32_t key, int* out_idx)
-{
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int nwaves = blockDim.x >> 6;
-    const uint32_t wmin = wave_min_u32(key);
-    if (lane == wave_first_lane_eq(key, wmin)) {
-        sh.key[par][wave] = wmin;
-        sh.idx[par][wave] = tid;
-    }
-    __syncthreads();
-    const uint32_t k2 = lane < nwaves ? sh.key[par][lane] : 0xFFFFFFFFu;
-    const uint32_t bmin = wave_min_u32(k2);
-    *out_idx = sh.idx[par][wave_first_lane_eq(k2, bmin)];
-    return bmin;
-}
-
 template <class Topo, int MODE, int POSREF>
 __global__ void __launch_bounds__(kResidentMaxThreads<Topo::J>())
     k_swarm_resident(const ChainConsts<Topo::J> cc, const SwarmIO io)
@@ -151,7 +77,7 @@ __global__ void __launch_bounds__(kResidentMaxThreads<Topo::J>())
     // Local-best positions, [d][lane]: read once per iteration by the update,
     // written on improvement; consecutive lanes hit consecutive banks.
     __shared__ float s_pb[D * BLOCK];
-    stage_swarm_inputs<J>(cc, io, b, sh);
+    stage_swarm_inputs<J>(cc, io.targets, io.start_pose, b, sh);
 
     Xorwow rng{0, 0, 0, 0, 0, 0};
     if (active) load_rng(rng, io.rng + b * P + tid);
@@ -300,38 +226,6 @@ static hipError_t run_evaluate(const ChainHost& ch, const EvalIO& io, hipStream_
     return hipGetLastError();
 }
 
-// Visit the kernel instantiation for (topology, J, mode).  Returns false when
-// the chain has no compiled variant.
-template <class F>
-static bool visit_topology(const ChainHost& ch, F&& f)
-{
-    switch (ch.topo) {
-    case TopoKind::Ref7:
-        f(TopoRef7{});
-        return true;
-#ifndef IKPSO_EXPERIMENT_REF7_ONLY
-    case TopoKind::SerialTip:
-        switch (ch.J) {
-        case 20: f(TopoSerialTip<20>{}); return true;
-        default: break;
-        }
-        [[fallthrough]];
-    case TopoKind::Generic:
-        switch (ch.J) {
-#define IKPSO_G(n) \
-    case n: f(TopoGeneric<n>{}); return true;
-            IKPSO_G(1) IKPSO_G(2) IKPSO_G(3) IKPSO_G(4) IKPSO_G(5) IKPSO_G(6) IKPSO_G(7) IKPSO_G(8) IKPSO_G(9)
-                IKPSO_G(10) IKPSO_G(12) IKPSO_G(16) IKPSO_G(20)
-#undef IKPSO_G
-        default: return false;
-        }
-#else
-    default: return false;
-#endif
-    }
-    return false;
-}
-
 int resident_max_threads(const ChainHost& ch)
 {
     int r = 0;
@@ -344,14 +238,14 @@ bool chain_supported(const ChainHost& ch)
     return visit_topology(ch, [](auto) {});
 }
 
-const char* kernel_name(const ChainHost& ch)
+const char* kernel_name(const ChainHost& ch, bool streaming)
 {
-    switch (ch.topo) {
-    case TopoKind::Ref7: return "swarm_resident<ref_tree7>";
-    case TopoKind::SerialTip:
-        return ch.J == 20 ? "swarm_resident<serial_tip20>" : "swarm_resident<generic>";
-    default: return "swarm_resident<generic>";
-    }
+    const bool spec = ch.topo == TopoKind::Ref7 || (ch.topo == TopoKind::SerialTip && ch.J == 20);
+    if (streaming)
+        return ch.topo == TopoKind::Ref7 ? "swarm_streaming<ref_tree7>"
+                                         : (spec ? "swarm_streaming<serial_tip20>" : "swarm_streaming<generic>");
+    return ch.topo == TopoKind::Ref7 ? "swarm_resident<ref_tree7>"
+                                     : (spec ? "swarm_resident<serial_tip20>" : "swarm_resident<generic>");
 }
 
 hipError_t launch_resident(const ChainHost& ch, int mode, const SwarmIO& io, hipStream_t stream)

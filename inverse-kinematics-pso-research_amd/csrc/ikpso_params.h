@@ -48,11 +48,34 @@ struct SwarmIO {
     int64_t num_swarms;
 };
 
-// Streaming (state-in-HBM) kernels: per-swarm global-best state, double
-// buffered by iteration parity.
-struct GBest {
-    uint32_t key;  // ordered fp32 key of the global-best fitness
-    int32_t idx;   // particle index of the global best
+// Streaming (state-in-HBM) kernels: one launch per PSO iteration over every
+// chunk of every swarm.  Launch t (0 = init, 1..I = iterations, I+1 =
+// finalize) writes its per-chunk argmin partials and the swarm's global-best
+// state to slot t&1 and reads the previous launch's from slot (t-1)&1, so no
+// workgroup ever reads what another workgroup of the same launch writes.
+constexpr int kStreamChunk = 256;  // particles per workgroup (4 waves)
+
+struct StreamIO {
+    float* state;               // [B][3][D][P]: x | v | pbest planes (the reference's particles layout)
+    float* pbf;                 // [B][P] local-best fitness
+    uint32_t* rng;              // SoA [6][B*P] generator words (d, v0..v4)
+    ikpso_rng_state* rng_aos;   // [B][P] caller/solver states: read at init, written at finalize
+    uint32_t* pkey;             // [2][B][C] chunk-min keys
+    int32_t* pidx;              // [2][B][C] chunk-min particle index
+    float* pvec;                // [2][B][C][D] chunk winner's pbest
+    uint32_t* gkey;             // [2][B] global-best key (0xFFFFFFFF before the first copy)
+    int32_t* gidx;              // [2][B]
+    float* gvec;                // [2][B][D] global-best vector
+    const float* targets;       // [B][E][3] or null
+    const float* start_pose;    // [B][D] or null
+    float* out_angles;          // [B][D]
+    float* out_fitness;         // [B] or null
+    float* out_residual;        // [B] or null
+    int64_t num_swarms;
+    int32_t P;
+    int32_t C;                  // chunks per swarm
+    int32_t t;                  // launch index (see above)
+    int32_t pad_;
 };
 
 }  // namespace ikpso

@@ -1,0 +1,286 @@
+// ikpso_stream.hip -- streaming variant of the swarm solve for swarms larger
+// than one workgroup (the visualiser's default N = 16384, src/Main.cpp:17) and
+// for long chains (BASELINE config 5: D = 60, P = 4096).
+//
+// Particle state lives in HBM in the reference's own SoA layout (per swarm
+// [3][D][P]: position | velocity | local best, src/kernel.cu:17-29); one
+// launch per PSO iteration covers every 256-particle chunk of every swarm, one
+// lane per particle, coalesced [d][particle] loads/stores.  The swarm argmin
+// (thrust::min_element, src/kernel.cu:297,315) is split across launches: each
+// workgroup publishes its chunk minimum (key, index, the winner's pbest) to
+// slot t&1, and every workgroup of the NEXT launch reduces those partials and
+// applies the `globalMin > currentGlobalMin` update (src/kernel.cu:318)
+// redundantly -- the kernel boundary is the only cross-workgroup ordering.
+#include <hip/hip_runtime.h>
+
+#include "ikpso_device.h"
+#include "ikpso_kernels.h"
+#include "ikpso_swarm.h"
+
+namespace ikpso {
+
+// Resolve the swarm's global best as of the end of launch t-1: reduce the C
+// chunk partials of slot (t-1)&1, compare with the global best of slot
+// (t-1)&1, stage the resulting vector in sh.g.  Uniform across the workgroup.
+// Workgroup 0 of each swarm publishes the result to slot t&1.
+template <int J>
+__device__ __forceinline__ uint32_t stream_resolve_gbest(const StreamIO& io, int64_t b, int c, SwarmShared<J>& sh)
+{
+    constexpr int D = 3 * J;
+    const int lane = threadIdx.x & 63;
+    const int prev = (io.t - 1) & 1, cur = io.t & 1;
+    const int64_t B = io.num_swarms;
+    const uint32_t* pk = io.pkey + ((int64_t)prev * B + b) * io.C;
+    const int32_t* pi = io.pidx + ((int64_t)prev * B + b) * io.C;
+    uint32_t best = 0xFFFFFFFFu;
+    int best_chunk = 0;
+    for (int base = 0; base < io.C; base += 64) {  // chunks in order: ties keep the lowest chunk
+        const uint32_t k = base + lane < io.C ? pk[base + lane] : 0xFFFFFFFFu;
+        const uint32_t m = wave_min_u32(k);
+        if (m < best) {
+            best = m;
+            best_chunk = base + wave_first_lane_eq(k, m);
+        }
+    }
+    const uint32_t gprev = io.gkey[(int64_t)prev * B + b];
+    const bool improved = best < gprev;
+    const float* src = improved ? io.pvec + (((int64_t)prev * B + b) * io.C + best_chunk) * D
+                                : io.gvec + ((int64_t)prev * B + b) * D;
+    for (int d = threadIdx.x; d < D; d += blockDim.x) sh.g[d] = src[d];
+    if (c == 0) {
+        if (threadIdx.x == 0) {
+            io.gkey[(int64_t)cur * B + b] = improved ? best : gprev;
+            io.gidx[(int64_t)cur * B + b] = improved ? pi[best_chunk] : io.gidx[(int64_t)prev * B + b];
+        }
+        for (int d = threadIdx.x; d < D; d += blockDim.x) io.gvec[((int64_t)cur * B + b) * D + d] = src[d];
+    }
+    return improved ? best : gprev;
+}
+
+// Chunk argmin of the local-best keys -> partial slot t&1; the winner lane
+// publishes its pbest vector (x if it improved in this launch, else from HBM).
+template <int J>
+__device__ __forceinline__ void stream_publish_chunk(const StreamIO& io, int64_t b, int c, SwarmShared<J>& sh,
+                                                     uint32_t key, bool improved_now, const float* x,
+                                                     const float* pb_plane, int i)
+{
+    constexpr int D = 3 * J;
+    int widx;
+    const uint32_t m = swarm_argmin<J>(sh, 0, key, &widx);
+    const int cur = io.t & 1;
+    const int64_t slot = ((int64_t)cur * io.num_swarms + b) * io.C + c;
+    if (threadIdx.x == 0) {
+        io.pkey[slot] = m;
+        io.pidx[slot] = c * kStreamChunk + widx;
+    }
+    if (threadIdx.x == widx) {
+        float* dst = io.pvec + slot * D;
+#pragma unroll
+        for (int d = 0; d < D; ++d) dst[d] = improved_now ? x[d] : pb_plane[(int64_t)d * io.P + i];
+    }
+}
+
+template <class Topo, int MODE, int POSREF>
+__global__ void __launch_bounds__(kStreamChunk) k_stream_init(const ChainConsts<Topo::J> cc, const StreamIO io)
+{
+    constexpr int J = Topo::J;
+    constexpr int D = 3 * J;
+    const int64_t b = blockIdx.x / io.C;
+    const int c = blockIdx.x % io.C;
+    const int i = c * kStreamChunk + threadIdx.x;
+    const bool active = i < io.P;
+    const int64_t P = io.P;
+    __shared__ SwarmShared<J> sh;
+    stage_swarm_inputs<J>(cc, io.targets, io.start_pose, b, sh);
+    __syncthreads();
+
+    float* X = io.state + b * 3 * D * P;
+    float* V = X + D * P;
+    float* PB = X + 2 * D * P;
+    float x[D];
+    float pbf = 0.0f;
+    if (active) {
+        // initParticlesKernel (src/kernel.cu:223-266) + initLocalBests (:191-200)
+        Xorwow rng;
+        load_rng(rng, io.rng_aos + b * P + i);
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            x[d] = sh.rest[d];
+            X[d * P + i] = x[d];
+            V[d * P + i] = __builtin_fmaf(rng.uniform(), 2.0f, -1.0f);
+            PB[d * P + i] = x[d];
+        }
+        pbf = fitness<Topo, MODE, POSREF>(cc, x, sh.rest, sh.tgt, nullptr);
+        io.pbf[b * P + i] = pbf;
+        const int64_t n = io.num_swarms * P, k = b * P + i;
+        io.rng[0 * n + k] = rng.d;
+        io.rng[1 * n + k] = rng.v0;
+        io.rng[2 * n + k] = rng.v1;
+        io.rng[3 * n + k] = rng.v2;
+        io.rng[4 * n + k] = rng.v3;
+        io.rng[5 * n + k] = rng.v4;
+    }
+    stream_publish_chunk<J>(io, b, c, sh, active ? ordered_key(pbf) : 0xFFFFFFFFu, true, x, PB, i);
+    if (c == 0 && threadIdx.x == 0) io.gkey[(int64_t)(io.t & 1) * io.num_swarms + b] = 0xFFFFFFFFu;
+}
+
+template <class Topo, int MODE, int POSREF>
+__global__ void __launch_bounds__(kStreamChunk) k_stream_step(const ChainConsts<Topo::J> cc, const StreamIO io)
+{
+    constexpr int J = Topo::J;
+    constexpr int D = 3 * J;
+    const int64_t b = blockIdx.x / io.C;
+    const int c = blockIdx.x % io.C;
+    const int i = c * kStreamChunk + threadIdx.x;
+    const bool active = i < io.P;
+    const int64_t P = io.P;
+    __shared__ SwarmShared<J> sh;
+    stage_swarm_inputs<J>(cc, io.targets, io.start_pose, b, sh);
+    stream_resolve_gbest<J>(io, b, c, sh);
+    __syncthreads();
+
+    float* X = io.state + b * 3 * D * P;
+    float* V = X + D * P;
+    float* PB = X + 2 * D * P;
+    float x[D];
+    float pbf = 0.0f;
+    bool improved = false;
+    if (active) {
+        const int64_t n = io.num_swarms * P, k = b * P + i;
+        Xorwow rng;
+        rng.d = io.rng[0 * n + k];
+        rng.v0 = io.rng[1 * n + k];
+        rng.v1 = io.rng[2 * n + k];
+        rng.v2 = io.rng[3 * n + k];
+        rng.v3 = io.rng[4 * n + k];
+        rng.v4 = io.rng[5 * n + k];
+        pbf = io.pbf[b * P + i];
+#pragma unroll
+        for (int d = 0; d < D; ++d) x[d] = X[d * P + i];
+        // simulateParticlesKernel (src/kernel.cu:153-189)
+        const float w = cc.w, c1 = cc.c1, c2 = cc.c2;
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            float v = V[d * P + i];
+            pso_update<MODE>(x[d], v, PB[d * P + i], sh.g[d], w, c1, c2, rng);
+            V[d * P + i] = v;
+        }
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            x[d] = clamp_ref(x[d], sh.lo[d], sh.hi[d]);
+            X[d * P + i] = x[d];
+        }
+        // updateLocalBests (src/kernel.cu:202-221)
+        const float f = fitness<Topo, MODE, POSREF>(cc, x, sh.rest, sh.tgt, nullptr);
+        if (f < pbf) {
+            improved = true;
+            pbf = f;
+            io.pbf[b * P + i] = f;
+#pragma unroll
+            for (int d = 0; d < D; ++d) PB[d * P + i] = x[d];
+        }
+        io.rng[0 * n + k] = rng.d;
+        io.rng[1 * n + k] = rng.v0;
+        io.rng[2 * n + k] = rng.v1;
+        io.rng[3 * n + k] = rng.v2;
+        io.rng[4 * n + k] = rng.v3;
+        io.rng[5 * n + k] = rng.v4;
+    }
+    stream_publish_chunk<J>(io, b, c, sh, active ? ordered_key(pbf) : 0xFFFFFFFFu, improved, x, PB, i);
+}
+
+template <class Topo, int MODE>
+__global__ void __launch_bounds__(kStreamChunk) k_stream_finalize(const ChainConsts<Topo::J> cc, const StreamIO io)
+{
+    constexpr int J = Topo::J;
+    constexpr int D = 3 * J;
+    const int64_t b = blockIdx.x / io.C;
+    const int c = blockIdx.x % io.C;
+    const int i = c * kStreamChunk + threadIdx.x;
+    const int64_t P = io.P;
+    __shared__ SwarmShared<J> sh;
+    stage_swarm_inputs<J>(cc, io.targets, io.start_pose, b, sh);
+    const uint32_t gkey = stream_resolve_gbest<J>(io, b, c, sh);
+    __syncthreads();
+    if (c == 0) {
+        // Coordinates result (updateGlobalBestCoordsKernel) + fitness + residual
+        for (int d = threadIdx.x; d < D; d += blockDim.x) io.out_angles[b * D + d] = sh.g[d];
+        if (threadIdx.x == 0 && io.out_fitness) io.out_fitness[b] = key_to_float(gkey);
+        if (io.out_residual && threadIdx.x < 64) {
+            float g[D];
+#pragma unroll
+            for (int d = 0; d < D; ++d) g[d] = sh.g[d];
+            const float r = residual<Topo, MODE>(cc, g, sh.tgt);
+            if (threadIdx.x == 0) io.out_residual[b] = r;
+        }
+    }
+    if (i < io.P) {  // generator states back to the caller's / solver's layout
+        const int64_t n = io.num_swarms * P, k = b * P + i;
+        Xorwow rng;
+        rng.d = io.rng[0 * n + k];
+        rng.v0 = io.rng[1 * n + k];
+        rng.v1 = io.rng[2 * n + k];
+        rng.v2 = io.rng[3 * n + k];
+        rng.v3 = io.rng[4 * n + k];
+        rng.v4 = io.rng[5 * n + k];
+        store_rng(rng, io.rng_aos + k);
+    }
+}
+
+template <class Topo, int MODE, int POSREF>
+static hipError_t run_stream(const ChainHost& ch, StreamIO io, int iterations, hipStream_t stream)
+{
+    const ChainConsts<Topo::J> cc = make_consts<Topo::J>(ch);
+    const dim3 grid((unsigned)(io.num_swarms * io.C)), threads(kStreamChunk);
+    io.t = 0;
+    hipLaunchKernelGGL((k_stream_init<Topo, MODE, POSREF>), grid, threads, 0, stream, cc, io);
+    for (int t = 1; t <= iterations; ++t) {
+        io.t = t;
+        hipLaunchKernelGGL((k_stream_step<Topo, MODE, POSREF>), grid, threads, 0, stream, cc, io);
+    }
+    io.t = iterations + 1;
+    hipLaunchKernelGGL((k_stream_finalize<Topo, MODE>), grid, threads, 0, stream, cc, io);
+    return hipGetLastError();
+}
+
+template <class Topo, int MODE>
+static hipError_t run_stream_posref(const ChainHost& ch, const StreamIO& io, int iterations, hipStream_t stream)
+{
+    if constexpr (Topo::kGeneric)
+        return run_stream<Topo, MODE, 2>(ch, io, iterations, stream);
+    else
+        return ch.use_posref ? run_stream<Topo, MODE, 1>(ch, io, iterations, stream)
+                             : run_stream<Topo, MODE, 0>(ch, io, iterations, stream);
+}
+
+hipError_t launch_stream(const ChainHost& ch, int mode, const StreamIO& io, int iterations, hipStream_t stream)
+{
+    if (io.num_swarms <= 0) return hipSuccess;
+    if (!ch.aux_dev || io.C != (io.P + kStreamChunk - 1) / kStreamChunk) return hipErrorInvalidValue;
+    hipError_t err = hipErrorInvalidValue;
+    const bool ok = visit_topology(ch, [&](auto topo) {
+        using T = decltype(topo);
+        if (mode == IKPSO_ARITH_REFERENCE)
+            err = run_stream_posref<T, IKPSO_ARITH_REFERENCE>(ch, io, iterations, stream);
+        else
+            err = run_stream_posref<T, IKPSO_ARITH_FAST>(ch, io, iterations, stream);
+    });
+    return ok ? err : hipErrorInvalidValue;
+}
+
+// Workspace bytes for B swarms of P particles and D angles (state excluded when
+// the caller provides it).
+size_t stream_workspace_bytes(int64_t B, int P, int D, bool with_state)
+{
+    const int64_t C = (P + kStreamChunk - 1) / kStreamChunk;
+    size_t n = 0;
+    if (with_state) n += sizeof(float) * (size_t)B * 3 * D * P + sizeof(float) * (size_t)B * P;
+    n += sizeof(uint32_t) * 6 * (size_t)B * P;           // rng SoA
+    n += (sizeof(uint32_t) + sizeof(int32_t)) * 2 * B * C;  // partial keys/idx
+    n += sizeof(float) * 2 * B * C * D;                   // partial vectors
+    n += (sizeof(uint32_t) + sizeof(int32_t)) * 2 * B;      // global best key/idx
+    n += sizeof(float) * 2 * B * D;                       // global best vector
+    return n + 8 * 256;                                   // alignment slack
+}
+
+}  // namespace ikpso

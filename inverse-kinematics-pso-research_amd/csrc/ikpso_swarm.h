@@ -1,0 +1,121 @@
+// ikpso_swarm.h -- device helpers shared by the resident and streaming swarm
+// kernels: per-swarm LDS staging, the swarm argmin, generator state I/O, and
+// the host-side dispatch over compiled topologies.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "ikpso_device.h"
+#include "ikpso_kernels.h"
+
+namespace ikpso {
+
+__device__ __forceinline__ void load_rng(Xorwow& r, const ikpso_rng_state* p)
+{
+    const uint32_t* q = reinterpret_cast<const uint32_t*>(p);
+    r.d = q[0];
+    r.v0 = q[1];
+    r.v1 = q[2];
+    r.v2 = q[3];
+    r.v3 = q[4];
+    r.v4 = q[5];
+}
+
+__device__ __forceinline__ void store_rng(const Xorwow& r, ikpso_rng_state* p)
+{
+    uint32_t* q = reinterpret_cast<uint32_t*>(p);
+    q[0] = r.d;
+    q[1] = r.v0;
+    q[2] = r.v1;
+    q[3] = r.v2;
+    q[4] = r.v3;
+    q[5] = r.v4;
+}
+
+// Per-swarm uniform constants staged in LDS.  They are read at their point of
+// use every iteration (an empty asm with a memory clobber at the top of the
+// iteration stops the compiler from hoisting them into registers): ~100
+// loop-invariant uniforms held in SGPRs/VGPRs across the loop spill, while a
+// broadcast ds_read costs one LDS cycle.
+template <int J>
+struct SwarmShared {
+    float lo[3 * J], hi[3 * J];  // clamp bounds
+    float rest[3 * J];           // warm start + angle-term reference
+    float tgt[3 * J];            // effector targets per node (k-1), 0 elsewhere
+    float g[3 * J];              // global-best vector
+    uint32_t key[2][16];         // per-wave argmin, double-buffered by parity
+    int32_t idx[2][16];
+};
+
+template <int J>
+__device__ __forceinline__ void stage_swarm_inputs(const ChainConsts<J>& cc, const float* targets,
+                                                   const float* start_pose, int64_t b, SwarmShared<J>& sh)
+{
+    constexpr int D = 3 * J;
+    const float* t = targets ? targets + b * (int64_t)cc.num_eff * 3 : nullptr;
+    for (int d = threadIdx.x; d < D; d += blockDim.x) {
+        sh.lo[d] = cc.lo[d];
+        sh.hi[d] = cc.hi[d];
+        sh.rest[d] = start_pose ? start_pose[b * D + d] : cc.rest[d];
+        const int s = cc.eff_slot[d / 3 + 1];
+        sh.tgt[d] = t ? (s >= 0 ? t[3 * s + d % 3] : 0.0f) : cc.tgt0[d];
+    }
+}
+
+__device__ __forceinline__ void compiler_fence() { asm volatile("" ::: "memory"); }
+
+// Swarm argmin of the local-best fitness keys, lowest particle index on ties
+// (thrust::min_element, src/kernel.cu:297,315).  One DPP wave min + ballot per
+// wave, a 16-entry LDS exchange, then every wave reduces the 16 entries
+// redundantly, so the result is uniform without a second barrier.
+template <int J>
+__device__ __forceinline__ uint32_t swarm_argmin(SwarmShared<J>& sh, int par, uint32_t key, int* out_idx)
+{
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int nwaves = blockDim.x >> 6;
+    const uint32_t wmin = wave_min_u32(key);
+    if (lane == wave_first_lane_eq(key, wmin)) {
+        sh.key[par][wave] = wmin;
+        sh.idx[par][wave] = tid;
+    }
+    __syncthreads();
+    const uint32_t k2 = lane < nwaves ? sh.key[par][lane] : 0xFFFFFFFFu;
+    const uint32_t bmin = wave_min_u32(k2);
+    *out_idx = sh.idx[par][wave_first_lane_eq(k2, bmin)];
+    return bmin;
+}
+
+// Visit the kernel instantiation for (topology, J, mode).  Returns false when
+// the chain has no compiled variant.
+template <class F>
+inline bool visit_topology(const ChainHost& ch, F&& f)
+{
+    switch (ch.topo) {
+    case TopoKind::Ref7:
+        f(TopoRef7{});
+        return true;
+#ifndef IKPSO_EXPERIMENT_REF7_ONLY
+    case TopoKind::SerialTip:
+        switch (ch.J) {
+        case 20: f(TopoSerialTip<20>{}); return true;
+        default: break;
+        }
+        [[fallthrough]];
+    case TopoKind::Generic:
+        switch (ch.J) {
+#define IKPSO_G(n) \
+    case n: f(TopoGeneric<n>{}); return true;
+            IKPSO_G(1) IKPSO_G(2) IKPSO_G(3) IKPSO_G(4) IKPSO_G(5) IKPSO_G(6) IKPSO_G(7) IKPSO_G(8) IKPSO_G(9)
+                IKPSO_G(10) IKPSO_G(12) IKPSO_G(16) IKPSO_G(20)
+#undef IKPSO_G
+        default: return false;
+        }
+#else
+    default: return false;
+#endif
+    }
+    return false;
+}
+
+
+}  // namespace ikpso

@@ -28,6 +28,10 @@ NODE_ORIGIN, NODE_EFFECTOR, NODE = 0, 1, 2  # src/Particle.h:10-15
 ARITH_FAST = 0
 ARITH_REFERENCE = 1
 
+KERNEL_AUTO = 0
+KERNEL_RESIDENT = 1
+KERNEL_STREAMING = 2
+
 # ------------------------------------------------------------ numpy layouts
 #: NodeCUDA (src/Particle.h:24-39), 88 bytes.
 NODE_DTYPE = np.dtype(
@@ -92,7 +96,7 @@ class SolverDesc(ctypes.Structure):
         ("pso", PSOConfig),
         ("fit", FitnessConfig),
         ("arith", ctypes.c_int32),
-        ("reserved0", ctypes.c_int32),
+        ("kernel", ctypes.c_int32),
         ("positions", ctypes.c_void_p),
         ("limit_weight", ctypes.c_float),
         ("reserved1", ctypes.c_float),

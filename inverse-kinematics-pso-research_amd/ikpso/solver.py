@@ -147,7 +147,7 @@ class BatchSolver:
 
     def __init__(self, chain: np.ndarray, particles: int, pso: PSOConfig = MAIN_PSO,
                  fit: FitnessConfig = MAIN_FITNESS, arith: str = "fast", positions=None,
-                 limit_weight: float = 0.0, soft_lo=None, soft_hi=None):
+                 limit_weight: float = 0.0, soft_lo=None, soft_hi=None, kernel: str = "auto"):
         self._lib = _abi.load()
         if chain.dtype != NODE_DTYPE:
             raise TypeError("chain must be an ikpso NODE_DTYPE array")
@@ -163,6 +163,8 @@ class BatchSolver:
         desc.pso = pso.c()
         desc.fit = fit.c()
         desc.arith = {"fast": _abi.ARITH_FAST, "reference": _abi.ARITH_REFERENCE}[arith]
+        desc.kernel = {"auto": _abi.KERNEL_AUTO, "resident": _abi.KERNEL_RESIDENT,
+                       "streaming": _abi.KERNEL_STREAMING}[kernel]
         desc.positions = _any_ptr(None if positions is None else np.asarray(positions, np.float32), keep)
         desc.limit_weight = float(limit_weight)
         desc.soft_lo = _any_ptr(None if soft_lo is None else np.asarray(soft_lo, np.float32), keep)

@@ -241,10 +241,47 @@ void orc_chain_matrices(const orc_node* chain, int node_count, const float* angl
 static inline float msq3(float x, float y, float z) { return (x * x) + (y * y) + (z * z); }
 static inline float msq4(float x, float y, float z, float w) { return (x * x) + (y * y) + (z * z) + (w * w); }
 
+/* Optional soft joint-limit penalty -- an EXTENSION (BASELINE config 5), not in
+ * the reference (which only clamps): f += limit_weight * sum_d over_d^2,
+ * over_d = max(x_d - soft_hi_d, soft_lo_d - x_d, 0), summed in d order. */
+typedef struct {
+    float limit_weight;
+    const float* soft_lo;
+    const float* soft_hi;
+} orc_penalty;
+
+static float penalty_term(const orc_penalty* pen, const float* angles, int dof)
+{
+    float p = 0.0f;
+    for (int d = 0; d < dof; d++) {
+        float over = fmaxf(fmaxf(angles[d] - pen->soft_hi[d], pen->soft_lo[d] - angles[d]), 0.0f);
+        p = p + over * over;
+    }
+    return pen->limit_weight * p;
+}
+
+static float fitness_pen(const orc_node* chain, int node_count, const float* positions, const float* angles,
+                         float angle_weight, float distance_weight, const orc_penalty* pen);
+
 /* calculateDistance (src/kernel.cu:64-151) with colliderCount = 0.
  * angles contiguous [D]; positions = host-filled arm positions (read at slot (ind-1)*4). */
 float orc_fitness(const orc_node* chain, int node_count, const float* positions, const float* angles,
                   float angle_weight, float distance_weight)
+{
+    return fitness_pen(chain, node_count, positions, angles, angle_weight, distance_weight, NULL);
+}
+
+float orc_fitness_ex(const orc_node* chain, int node_count, const float* positions, const float* angles,
+                     float angle_weight, float distance_weight, float limit_weight, const float* soft_lo,
+                     const float* soft_hi)
+{
+    orc_penalty pen = {limit_weight, soft_lo, soft_hi};
+    return fitness_pen(chain, node_count, positions, angles, angle_weight, distance_weight,
+                       (limit_weight != 0.0f && soft_lo && soft_hi) ? &pen : NULL);
+}
+
+static float fitness_pen(const orc_node* chain, int node_count, const float* positions, const float* angles,
+                         float angle_weight, float distance_weight, const orc_penalty* pen)
 {
     const int dof = 3 * (node_count - 1);
     float rot_diff = 0.0f, pos_diff = 0.0f, distance = 0.0f;
@@ -274,16 +311,18 @@ float orc_fitness(const orc_node* chain, int node_count, const float* positions,
     }
     if (mp != mats) free(mp);
     const float jn = (float)(dof / 3);
-    return distance + distance_weight / jn * pos_diff + angle_weight / jn * rot_diff;
+    float f = distance + distance_weight / jn * pos_diff + angle_weight / jn * rot_diff;
+    if (pen) f = f + penalty_term(pen, angles, dof);
+    return f;
 }
 
 static float fitness_soa(const orc_node* chain, int node_count, const float* positions, const float* particles,
-                         int64_t count, int64_t i, float aw, float dw)
+                         int64_t count, int64_t i, float aw, float dw, const orc_penalty* pen)
 {
     const int dof = 3 * (node_count - 1);
     float ang[3 * 64];
     for (int d = 0; d < dof; d++) ang[d] = particles[pidx(count, i, 0, d, dof)];
-    return orc_fitness(chain, node_count, positions, ang, aw, dw);
+    return fitness_pen(chain, node_count, positions, ang, aw, dw, pen);
 }
 
 /* Node world positions (xyz) for nodes 1..J: out[3*(k-1)+c]. */
@@ -328,9 +367,34 @@ static int64_t argmin_first(const float* v, int64_t n)
 /* calculatePSO (src/kernel.cu:279-327), colliderCount = 0.
  * particles: [3][dof][size] SoA (position, velocity, localBest); bests[size];
  * randoms[size]; result[dof].  Returns 0. */
+static int calculate_pso_pen(float* particles, const float* positions, float* bests, orc_rng* randoms,
+                             int64_t size, const orc_node* chain, int node_count, float inertia, float local,
+                             float global, int iterations, float angle_weight, float distance_weight,
+                             float* result, const orc_penalty* pen);
+
 int orc_calculate_pso(float* particles, const float* positions, float* bests, orc_rng* randoms, int64_t size,
                       const orc_node* chain, int node_count, float inertia, float local, float global,
                       int iterations, float angle_weight, float distance_weight, float* result)
+{
+    return calculate_pso_pen(particles, positions, bests, randoms, size, chain, node_count, inertia, local, global,
+                             iterations, angle_weight, distance_weight, result, NULL);
+}
+
+int orc_calculate_pso_ex(float* particles, const float* positions, float* bests, orc_rng* randoms, int64_t size,
+                         const orc_node* chain, int node_count, float inertia, float local, float global,
+                         int iterations, float angle_weight, float distance_weight, float* result,
+                         float limit_weight, const float* soft_lo, const float* soft_hi)
+{
+    orc_penalty pen = {limit_weight, soft_lo, soft_hi};
+    return calculate_pso_pen(particles, positions, bests, randoms, size, chain, node_count, inertia, local, global,
+                             iterations, angle_weight, distance_weight, result,
+                             (limit_weight != 0.0f && soft_lo && soft_hi) ? &pen : NULL);
+}
+
+static int calculate_pso_pen(float* particles, const float* positions, float* bests, orc_rng* randoms,
+                             int64_t size, const orc_node* chain, int node_count, float inertia, float local,
+                             float global, int iterations, float angle_weight, float distance_weight,
+                             float* result, const orc_penalty* pen)
 {
     const int dof = 3 * (node_count - 1);
     const int64_t n = size;
@@ -350,7 +414,7 @@ int orc_calculate_pso(float* particles, const float* positions, float* bests, or
     }
     /* initLocalBests */
     for (int64_t i = 0; i < n; i++)
-        bests[i] = fitness_soa(chain, node_count, positions, particles, n, i, angle_weight, distance_weight);
+        bests[i] = fitness_soa(chain, node_count, positions, particles, n, i, angle_weight, distance_weight, pen);
 
     int64_t g = argmin_first(bests, n);
     for (int d = 0; d < dof; d++) result[d] = particles[pidx(n, g, 2, d, dof)];
@@ -378,7 +442,7 @@ int orc_calculate_pso(float* particles, const float* positions, float* bests, or
         }
         /* updateLocalBests (src/kernel.cu:202-221) */
         for (int64_t i = 0; i < n; i++) {
-            float f = fitness_soa(chain, node_count, positions, particles, n, i, angle_weight, distance_weight);
+            float f = fitness_soa(chain, node_count, positions, particles, n, i, angle_weight, distance_weight, pen);
             if (f < bests[i]) {
                 bests[i] = f;
                 for (int d = 0; d < dof; d++) particles[pidx(n, i, 2, d, dof)] = particles[pidx(n, i, 0, d, dof)];
@@ -401,14 +465,18 @@ int orc_calculate_pso(float* particles, const float* positions, float* bests, or
  * warm start + angle-term reference, as Node::ToCUDA does per frame).
  * rng: [B][P] states, persisting across calls.
  * Outputs: angles[B][D], fitness[B], residual[B] (residual may be NULL).
+ * limit_weight/soft_lo/soft_hi: optional penalty extension (0/NULL = off).
  * Parallel over swarms with OpenMP (threads <= 0: runtime default). */
 int orc_solve_batch(const orc_node* chain, int node_count, const float* targets, const float* start_pose,
                     int64_t num_swarms, int particles_per_swarm, int iterations, float inertia, float local,
                     float global, float angle_weight, float distance_weight, const float* positions,
-                    orc_rng* rng, float* out_angles, float* out_fitness, float* out_residual, int threads)
+                    orc_rng* rng, float* out_angles, float* out_fitness, float* out_residual, int threads,
+                    float limit_weight, const float* soft_lo, const float* soft_hi)
 {
     const int dof = 3 * (node_count - 1);
     const int64_t P = particles_per_swarm;
+    orc_penalty pen = {limit_weight, soft_lo, soft_hi};
+    const orc_penalty* penp = (limit_weight != 0.0f && soft_lo && soft_hi) ? &pen : NULL;
     int num_eff = 0;
     for (int k = 1; k < node_count; k++) num_eff += chain[k].node_type == ORC_EFFECTOR;
     if (node_count > 64 || node_count < 2) return 1;
@@ -442,8 +510,8 @@ int orc_solve_batch(const orc_node* chain, int node_count, const float* targets,
             }
         }
         float* res = out_angles + b * dof;
-        orc_calculate_pso(parts, positions, bests, rng + b * P, P, lc, node_count, inertia, local, global,
-                          iterations, angle_weight, distance_weight, res);
+        calculate_pso_pen(parts, positions, bests, rng + b * P, P, lc, node_count, inertia, local, global,
+                          iterations, angle_weight, distance_weight, res, penp);
         float gmin = bests[0];
         for (int64_t i = 1; i < P; i++)
             if (bests[i] < gmin) gmin = bests[i];

@@ -57,6 +57,8 @@ def load():
             "orc_uniform_stream": (None, [_P, _P, ctypes.c_int]),
             "orc_chain_matrices": (None, [_P, ctypes.c_int, _P, _P]),
             "orc_fitness": (ctypes.c_float, [_P, ctypes.c_int, _P, _P, ctypes.c_float, ctypes.c_float]),
+            "orc_fitness_ex": (ctypes.c_float, [_P, ctypes.c_int, _P, _P, ctypes.c_float, ctypes.c_float,
+                                                ctypes.c_float, _P, _P]),
             "orc_node_positions": (None, [_P, ctypes.c_int, _P, _P]),
             "orc_residual": (ctypes.c_float, [_P, ctypes.c_int, _P]),
             "orc_calculate_pso": (
@@ -64,10 +66,16 @@ def load():
                 [_P, _P, _P, _P, ctypes.c_int64, _P, ctypes.c_int, ctypes.c_float, ctypes.c_float, ctypes.c_float,
                  ctypes.c_int, ctypes.c_float, ctypes.c_float, _P],
             ),
+            "orc_calculate_pso_ex": (
+                ctypes.c_int,
+                [_P, _P, _P, _P, ctypes.c_int64, _P, ctypes.c_int, ctypes.c_float, ctypes.c_float, ctypes.c_float,
+                 ctypes.c_int, ctypes.c_float, ctypes.c_float, _P, ctypes.c_float, _P, _P],
+            ),
             "orc_solve_batch": (
                 ctypes.c_int,
                 [_P, ctypes.c_int, _P, _P, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_float,
-                 ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float, _P, _P, _P, _P, _P, ctypes.c_int],
+                 ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float, _P, _P, _P, _P, _P, ctypes.c_int,
+                 ctypes.c_float, _P, _P],
             ),
         }
         for name, (res, args) in sig.items():
@@ -122,11 +130,17 @@ def node_positions(chain, angles) -> np.ndarray:
     return out
 
 
-def fitness(chain, angles, angle_weight=3.0, distance_weight=0.0, positions=None) -> np.float32:
+def _f32(x):
+    return None if x is None else np.ascontiguousarray(x, dtype=np.float32)
+
+
+def fitness(chain, angles, angle_weight=3.0, distance_weight=0.0, positions=None, limit_weight=0.0, soft_lo=None,
+            soft_hi=None) -> np.float32:
     c = _chain(chain)
-    a = np.ascontiguousarray(angles, dtype=np.float32)
-    pos = None if positions is None else np.ascontiguousarray(positions, dtype=np.float32)
-    return np.float32(load().orc_fitness(_p(c), c.shape[0], _p(pos), _p(a), angle_weight, distance_weight))
+    a = _f32(angles)
+    pos, lo, hi = _f32(positions), _f32(soft_lo), _f32(soft_hi)
+    return np.float32(load().orc_fitness_ex(_p(c), c.shape[0], _p(pos), _p(a), angle_weight, distance_weight,
+                                            limit_weight, _p(lo), _p(hi)))
 
 
 def residual(chain, angles) -> np.float32:
@@ -136,7 +150,8 @@ def residual(chain, angles) -> np.float32:
 
 
 def calculate_pso(chain, size: int, randoms: np.ndarray, inertia=0.5, local=0.5, glob=1.25, iterations=15,
-                  angle_weight=3.0, distance_weight=0.0, positions=None):
+                  angle_weight=3.0, distance_weight=0.0, positions=None, limit_weight=0.0, soft_lo=None,
+                  soft_hi=None):
     """One reference solve.  Advances `randoms` in place.
     Returns (result [D], particles [3, D, size], bests [size])."""
     c = _chain(chain)
@@ -145,13 +160,16 @@ def calculate_pso(chain, size: int, randoms: np.ndarray, inertia=0.5, local=0.5,
     bests = np.zeros(size, dtype=np.float32)
     res = np.zeros(D, dtype=np.float32)
     pos = None if positions is None else np.ascontiguousarray(positions, dtype=np.float32)
-    load().orc_calculate_pso(_p(parts), _p(pos), _p(bests), _p(randoms), int(size), _p(c), c.shape[0], inertia,
-                             local, glob, int(iterations), angle_weight, distance_weight, _p(res))
+    lo, hi = _f32(soft_lo), _f32(soft_hi)
+    load().orc_calculate_pso_ex(_p(parts), _p(pos), _p(bests), _p(randoms), int(size), _p(c), c.shape[0], inertia,
+                                local, glob, int(iterations), angle_weight, distance_weight, _p(res), limit_weight,
+                                _p(lo), _p(hi))
     return res, parts, bests
 
 
 def solve_batch(chain, targets, start_pose, particles: int, iterations: int, rng: np.ndarray, inertia=0.5,
-                local=0.5, glob=1.25, angle_weight=3.0, distance_weight=0.0, positions=None, threads: int = 0):
+                local=0.5, glob=1.25, angle_weight=3.0, distance_weight=0.0, positions=None, threads: int = 0,
+                limit_weight=0.0, soft_lo=None, soft_hi=None):
     """B independent reference solves (OpenMP over swarms).  rng: [B*P] states, advanced in place.
     Returns (angles [B, D], fitness [B], residual [B])."""
     c = _chain(chain)
@@ -163,9 +181,10 @@ def solve_batch(chain, targets, start_pose, particles: int, iterations: int, rng
     ang = np.zeros((B, D), dtype=np.float32)
     fit = np.zeros(B, dtype=np.float32)
     res = np.zeros(B, dtype=np.float32)
+    lo, hi = _f32(soft_lo), _f32(soft_hi)
     err = load().orc_solve_batch(_p(c), c.shape[0], _p(t), _p(sp), B, int(particles), int(iterations), inertia,
                                  local, glob, angle_weight, distance_weight, _p(pos), _p(rng), _p(ang), _p(fit),
-                                 _p(res), int(threads))
+                                 _p(res), int(threads), limit_weight, _p(lo), _p(hi))
     if err:
         raise RuntimeError(f"orc_solve_batch failed ({err})")
     return ang, fit, res

@@ -284,3 +284,78 @@ def test_empty_and_invalid(device, scene_chain):
     with pytest.raises(ikpso.IkpsoError):
         s.solve(torch.zeros((3, 3, 3), device="cuda"), iterations=3)  # beyond seeded capacity
     s.close()
+
+
+# ------------------------------------------------------ streaming kernels
+@pytest.mark.parametrize("arith", ["fast", "reference"])
+@pytest.mark.parametrize("P,I", [(2048, 0), (2048, 1), (1500, 20)])
+def test_streaming_compat_vs_oracle(oracle, device, scene_chain, monkeypatch, arith, P, I):
+    """P > 1024 takes the streaming kernels automatically (state in the caller's particles buffer)."""
+    monkeypatch.setenv("IKPSO_ARITH", arith)
+    res, parts, bests, r = run_compat(scene_chain, P, I, arith)
+    ostate = oracle.init_generators(P, 0)
+    ores, oparts, obests = oracle.calculate_pso(scene_chain, P, ostate, iterations=I)
+    assert np.array_equal(r[:, :6], rng_words(ostate))
+    if arith == "reference":
+        assert np.array_equal(res, ores) and np.array_equal(parts, oparts) and np.array_equal(bests, obests)
+    assert np.max(np.abs(res - ores)) < 1e-4
+    assert abs(bests.min() - obests.min()) / obests.min() < 1e-5
+
+
+@pytest.mark.parametrize("arith", ["fast", "reference"])
+@pytest.mark.parametrize("P,I", [(256, 20), (1024, 30), (100, 7)])
+def test_streaming_equals_resident(device, scene_chain, monkeypatch, arith, P, I):
+    """The two kernel families run the same device arithmetic: identical bits."""
+    monkeypatch.setenv("IKPSO_ARITH", arith)
+    monkeypatch.setenv("IKPSO_KERNEL", "resident")
+    a = run_compat(scene_chain, P, I, arith)
+    monkeypatch.setenv("IKPSO_KERNEL", "streaming")
+    b = run_compat(scene_chain, P, I, arith)
+    for x, y in zip(a, b):
+        assert np.array_equal(x, y)
+
+
+def test_visualiser_default_swarm(oracle, device, scene_chain, monkeypatch):
+    """The visualiser's own call: N = 16384, PSOConfig(0.5, 0.5, 1.25, 15) (src/Main.cpp:17,130)."""
+    monkeypatch.setenv("IKPSO_ARITH", "reference")
+    P, I = 16384, 15
+    res, parts, bests, r = run_compat(scene_chain, P, I, "reference")
+    ostate = oracle.init_generators(P, 0)
+    ores, oparts, obests = oracle.calculate_pso(scene_chain, P, ostate, iterations=I)
+    assert np.array_equal(res, ores) and np.array_equal(bests, obests)
+    assert np.array_equal(r[:, :6], rng_words(ostate))
+
+
+def test_batch_streaming_equals_resident(device, batch_case):
+    wl, B, P, I, tg, oang, ofit, ores = batch_case
+    out = []
+    for kern in ("resident", "streaming"):
+        s = ikpso.BatchSolver(wl.chain, P, pso=wl.pso, kernel=kern)
+        s.seed(B)
+        out.append([t.cpu().numpy() for t in s.solve(dev(tg), iterations=I)])
+        assert kern in s.kernel
+        s.close()
+    for x, y in zip(*out):
+        assert np.array_equal(x, y)
+
+
+@pytest.mark.parametrize("arith", ["fast", "reference"])
+def test_config5_chain_with_penalty(oracle, device, arith):
+    """BASELINE config 5 shape at test size: 20-joint serial chain (D = 60), tip
+    effector, soft joint-limit penalty (extension), streaming kernels."""
+    wl = ikpso.workload(5)
+    B, P, I = 3, 512, 10
+    tg = wl.targets(0, B)
+    s = ikpso.BatchSolver(wl.chain, P, pso=ikpso.PSOConfig(0.5, 0.5, 1.25, I), arith=arith,
+                          limit_weight=wl.limit_weight, soft_lo=wl.soft_lo, soft_hi=wl.soft_hi)
+    assert "streaming" in s.kernel and "serial_tip20" in s.kernel
+    s.seed(B)
+    ang, fit, res = (t.cpu().numpy() for t in s.solve(dev(tg), iterations=I))
+    ostate = oracle.init_generators(B * P, 0)
+    oang, ofit, ores = oracle.solve_batch(wl.chain, tg, None, P, I, ostate, limit_weight=wl.limit_weight,
+                                          soft_lo=wl.soft_lo, soft_hi=wl.soft_hi, threads=4)
+    if arith == "reference":
+        assert np.array_equal(ang, oang) and np.array_equal(fit, ofit)
+    assert np.max(np.abs(fit - ofit) / ofit) < 1e-4
+    assert np.max(np.abs(res - ores)) < 1e-3
+    s.close()
