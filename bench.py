@@ -28,8 +28,8 @@ sys.path.insert(0, str(ROOT / "inverse-kinematics-pso-research_amd"))
 HBM_PEAK_GBS = 8000.0
 CUS, SIMDS, LANES_PER_CLK, CLOCK_GHZ = 256, 4, 32, 2.4
 VALU_PEAK_TINSTR = CUS * SIMDS * LANES_PER_CLK * CLOCK_GHZ / 1e3  # lane-instructions/s, 78.6 T
-# algorithmic bytes per particle-update = 20*D + 8 (x, v, pbest read; x, v written; pbest fitness r/w)
-ALG_BYTES_PER_UPDATE_D21 = 20 * 21 + 8
+# algorithmic bytes per particle-update = 20*D + 8 (x, v, pbest read; x, v written; pbest
+# fitness r/w): 428 B at D = 21, 1208 B at D = 60
 
 
 def parse():
@@ -37,9 +37,12 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--swarms-per-gpu", type=int, default=4096)
-    ap.add_argument("--particles", type=int, default=1024)
-    ap.add_argument("--iterations", type=int, default=500)
+    ap.add_argument("--config", type=int, default=3, choices=[3, 4, 5],
+                    help="BASELINE config: 3 = 4096 targets per GPU (default), 4 = 65536 targets over all GPUs, "
+                         "5 = 20-joint chain, 8192 targets over all GPUs, 4096 particles, penalty")
+    ap.add_argument("--swarms-per-gpu", type=int, default=None)
+    ap.add_argument("--particles", type=int, default=None)
+    ap.add_argument("--iterations", type=int, default=None)
     ap.add_argument("--arith", choices=["fast", "reference"], default="fast")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU baseline sample (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=16)
@@ -105,13 +108,20 @@ def main():
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
 
-    wl = ikpso.workload(3)
-    P, I = args.particles, args.iterations
-    Bl = args.swarms_per_gpu
+    wl = ikpso.workload(args.config)
+    P = args.particles or wl.particles
+    I = args.iterations or wl.iterations
+    if args.swarms_per_gpu:
+        Bl = args.swarms_per_gpu
+    elif args.config == 3:
+        Bl = wl.swarms                      # weak scaling: 4096 per GPU
+    else:
+        Bl = -(-wl.swarms // world)         # configs 4/5: the named total over all GPUs
     total = Bl * world
     first = rank * Bl
     targets = torch.from_numpy(wl.targets(first, Bl)).to(dev)
-    solver = ikpso.BatchSolver(wl.chain, P, pso=ikpso.PSOConfig(0.5, 0.5, 1.25, I), arith=args.arith)
+    solver = ikpso.BatchSolver(wl.chain, P, pso=ikpso.PSOConfig(0.5, 0.5, 1.25, I), arith=args.arith,
+                               limit_weight=wl.limit_weight, soft_lo=wl.soft_lo, soft_hi=wl.soft_hi)
     solver.seed(Bl, seed_base=0, first_swarm=first)
     D = solver.dof
     out = (torch.empty((Bl, D), device=dev), torch.empty((Bl,), device=dev), torch.empty((Bl,), device=dev))
@@ -158,7 +168,7 @@ def main():
     mean_res = float(res[:, D + 1].mean())
 
     single_ms = None
-    if rank == 0:
+    if rank == 0 and args.config != 5:
         s2 = ikpso.BatchSolver(wl.chain, P, pso=ikpso.PSOConfig(0.5, 0.5, 1.25, I), arith=args.arith)
         s2.seed(1)
         tg1 = targets[:1].contiguous()
@@ -176,8 +186,10 @@ def main():
     if rank == 0:
         ups_launch = Bl * P * I
         kern_s = kern_ms / 1e3
-        alg_gbs = ups_launch * ALG_BYTES_PER_UPDATE_D21 / kern_s / 1e9
-        vpu = valu_per_update()
+        alg_bytes = 20 * D + 8
+        alg_gbs = ups_launch * alg_bytes / kern_s / 1e9
+        streaming = "streaming" in solver.kernel
+        vpu = None if streaming else valu_per_update()
         valu = None
         if vpu:
             ach = ups_launch * vpu["valu_lane_instr_per_update"] / kern_s / 1e12
@@ -191,21 +203,22 @@ def main():
             "unit": valu["unit"] if valu else "GB/s",
             "frac": valu["frac"] if valu else round(alg_gbs / HBM_PEAK_GBS, 4),
             "traffic": round(vpu["hbm_bytes_per_update"] * ups_launch) if vpu else None,
-            "kernel": "k_swarm_resident<TopoRef7,FAST> (one launch = one batch)",
+            "kernel": solver.kernel + (" (I+2 launches per batch)" if streaming else " (one launch = one batch)"),
             "kernel_ms": round(kern_ms, 3),
             "hbm_algorithmic": {
                 "achieved": round(alg_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(alg_gbs / HBM_PEAK_GBS, 4),
-                "bytes_per_update": ALG_BYTES_PER_UPDATE_D21,
+                "bytes_per_update": alg_bytes,
                 "note": "SURVEY §8(d) north-star formulation (x/v/pbest streamed through HBM every iteration); "
                         "this kernel keeps them on chip, so the figure can exceed 1 and the binding roof is VALU",
             },
         }
         cpu = None
-        if world == 1 and args.cpu_seconds > 0:
+        if world == 1 and args.cpu_seconds > 0 and args.config == 3:
             cpu = cpu_baseline(wl, args.cpu_seconds, args.cpu_threads)
         line = {
-            "metric": "PSO particle-updates/sec + IK solves/sec, 7-DOF 1024-particle swarm",
+            "metric": "PSO particle-updates/sec + IK solves/sec, 7-DOF 1024-particle swarm" if args.config != 5
+                      else "PSO particle-updates/sec + IK solves/sec, 20-DOF 4096-particle swarm (config 5)",
             "value": value,
             "unit": "particle-updates/s",
             "n_gpus": world,
@@ -216,9 +229,10 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic (seeded targets: reset targets + U[-0.25,0.25]^3 per effector)",
+            "data": "synthetic (seeded targets: reset targets + U[-0.25,0.25]^3 per effector)" if args.config != 5
+                    else "synthetic (seeded targets uniform in a radius-2..4 shell)",
             "config": {
-                "workload": "config3: 7-joint (21-DOF) reference scene, 1024-particle swarms, 500 PSO iterations, "
+                "workload": f"config{args.config}: {wl.description}; {P} particles, {I} PSO iterations, "
                             f"{Bl} targets per GPU ({total} total)",
                 "swarms_per_gpu": Bl, "total_swarms": total, "particles": P, "iterations": I, "dof": D,
                 "parallelism": f"dp{world} (swarm shards) + RCCL all-gather of results" if world > 1

@@ -19,7 +19,7 @@
 #define IKPSO_SCHED_NODE 0
 #endif
 #ifndef IKPSO_SCHED_DIM
-#define IKPSO_SCHED_DIM 0
+#define IKPSO_SCHED_DIM 1
 #endif
 
 namespace ikpso {
@@ -228,9 +228,14 @@ __device__ __forceinline__ Frame child_frame_reference(const Frame& P, float a, 
 {
 #pragma clang fp contract(off)
     float sa, ca, sb, cb, sc, cc;
+    // one fp64 evaluation at a time: interleaving three keeps ~3x the 64-bit
+    // temporaries live and spills the particle state
     sincos_reference(a, &sa, &ca);
+    __builtin_amdgcn_sched_barrier(0);
     sincos_reference(b, &sb, &cb);
+    __builtin_amdgcn_sched_barrier(0);
     sincos_reference(c, &sc, &cc);
+    __builtin_amdgcn_sched_barrier(0);
     // A2 = Rx(a) * Ry(b)
     const float a00 = cb, a02 = sb;
     const float a10 = sa * sb, a11 = ca, a12 = (-sa) * cb;
@@ -274,21 +279,32 @@ __device__ __forceinline__ Frame child_frame(const Frame& P, float a, float b, f
 // `tgt` holds the effector targets per node (3 floats at 3*(k-1)); for the
 // generic topology non-effector nodes carry weight 0 and target 0, and adding
 // the resulting +0 leaves a finite sum unchanged bit for bit.
-// POSREF: 0 = distance term off (distanceWeight == 0), 1 = on, 2 = runtime flag.
-template <class Topo, int MODE, int POSREF>
-__device__ __forceinline__ float fitness(const ChainConsts<Topo::J>& cc, const float* x, const float* rest,
-                                         const float* tgt, float* node_pos /* [3J] or nullptr */)
-{
-#pragma clang fp contract(off)
-    constexpr int J = Topo::J;
+// TERMS: which optional terms are compiled in -- kTermPosRef (distanceWeight
+// != 0: the positions[] term), kTermPenalty (soft joint limits), or
+// kTermRuntime (generic kernels: both decided by runtime flags).
+constexpr int kTermPosRef = 1, kTermPenalty = 2, kTermRuntime = 4;
+
+template <class Topo, int MODE, int TERMS>
+struct FitnessAcc {
+    static constexpr int J = Topo::J;
     Frame F[J + 1];
-    F[0] = origin_frame(cc.m0);
-    float rot_diff = 0.0f, pos_diff = 0.0f, distance = 0.0f;
-    const bool posref = POSREF == 1 || (POSREF == 2 && cc.use_posref);
-#pragma unroll
-    for (int k = 1; k <= J; ++k) {
+    float rot_diff, pos_diff, distance, pen;
+    bool posref, penalty;
+
+    __device__ __forceinline__ explicit FitnessAcc(const ChainConsts<J>& cc)
+        : rot_diff(0.0f), pos_diff(0.0f), distance(0.0f), pen(0.0f),
+          posref((TERMS & kTermPosRef) || ((TERMS & kTermRuntime) && cc.use_posref)),
+          penalty((TERMS & kTermPenalty) || ((TERMS & kTermRuntime) && cc.use_penalty))
+    {
+        F[0] = origin_frame(cc.m0);
+    }
+
+    // Node k (1..J) with its three Euler angles; nodes must come in index order.
+    __device__ __forceinline__ void node(const ChainConsts<J>& cc, int k, float a, float b, float c,
+                                         const float* rest, const float* tgt, float* node_pos)
+    {
+#pragma clang fp contract(off)
         const int pk = Topo::kGeneric ? cc.parent[k] : Topo::parent(k);
-        const float a = x[3 * (k - 1) + 0], b = x[3 * (k - 1) + 1], c = x[3 * (k - 1) + 2];
         F[k] = child_frame<MODE>(F[pk], a, b, c, cc.len[k]);
         const float dx = rest[3 * (k - 1) + 0] - a, dy = rest[3 * (k - 1) + 1] - b, dz = rest[3 * (k - 1) + 2] - c;
         if constexpr (MODE == IKPSO_ARITH_REFERENCE) {
@@ -316,29 +332,47 @@ __device__ __forceinline__ float fitness(const ChainConsts<Topo::J>& cc, const f
                 distance = distance + ((ex * ex + ey * ey) + ez * ez) * cc.eff_w[k];
             }
         }
+        if (penalty) {  // soft joint-limit penalty (extension, BASELINE config 5), d order
+            const float ang[3] = {a, b, c};
+#pragma unroll
+            for (int ax = 0; ax < 3; ++ax) {
+                const int d = 3 * (k - 1) + ax;
+                const float slo = cc.aux[4 * J + d], shi = cc.aux[7 * J + d];
+                const float over = fmaxf(fmaxf(ang[ax] - shi, slo - ang[ax]), 0.0f);
+                pen = pen + over * over;
+            }
+        }
         if (node_pos) {
             node_pos[3 * (k - 1) + 0] = F[k].px;
             node_pos[3 * (k - 1) + 1] = F[k].py;
             node_pos[3 * (k - 1) + 2] = F[k].pz;
         }
+    }
+
+    __device__ __forceinline__ float finish(const ChainConsts<J>& cc) const
+    {
+#pragma clang fp contract(off)
+        float f = posref ? (distance + cc.dw_j * pos_diff) + cc.aw_j * rot_diff : distance + cc.aw_j * rot_diff;
+        if (penalty) f = f + cc.lim_w * pen;
+        return f;
+    }
+};
+
+template <class Topo, int MODE, int TERMS>
+__device__ __forceinline__ float fitness(const ChainConsts<Topo::J>& cc, const float* x, const float* rest,
+                                         const float* tgt, float* node_pos /* [3J] or nullptr */)
+{
+    FitnessAcc<Topo, MODE, TERMS> acc(cc);
+#pragma unroll
+    for (int k = 1; k <= Topo::J; ++k) {
+        acc.node(cc, k, x[3 * (k - 1) + 0], x[3 * (k - 1) + 1], x[3 * (k - 1) + 2], rest, tgt, node_pos);
 #if IKPSO_SCHED_NODE
         // One node at a time: keeps the scheduler from hoisting all 3J
         // independent sincos evaluations to the top of the evaluation.
         __builtin_amdgcn_sched_barrier(0);
 #endif
     }
-    float f = posref ? (distance + cc.dw_j * pos_diff) + cc.aw_j * rot_diff : distance + cc.aw_j * rot_diff;
-    if (cc.use_penalty) {  // soft joint-limit penalty (extension, BASELINE config 5)
-        float pen = 0.0f;
-#pragma unroll
-        for (int d = 0; d < 3 * J; ++d) {
-            const float slo = cc.aux[4 * J + d], shi = cc.aux[7 * J + d];
-            const float over = fmaxf(fmaxf(x[d] - shi, slo - x[d]), 0.0f);
-            pen = pen + over * over;
-        }
-        f = f + cc.lim_w * pen;
-    }
-    return f;
+    return acc.finish(cc);
 }
 
 // Sum over effectors of the Euclidean distance to target (checkDistance,

@@ -61,7 +61,7 @@ hipError_t launch_init_generators(ikpso_rng_state* st, int64_t count, uint64_t s
 }
 
 // ------------------------------------------------------- resident swarm kernel
-template <class Topo, int MODE, int POSREF>
+template <class Topo, int MODE, int TERMS>
 __global__ void __launch_bounds__(kResidentMaxThreads<Topo::J>())
     k_swarm_resident(const ChainConsts<Topo::J> cc, const SwarmIO io)
 {
@@ -93,7 +93,7 @@ __global__ void __launch_bounds__(kResidentMaxThreads<Topo::J>())
         s_pb[d * BLOCK + tid] = x[d];
     }
     // initLocalBests (src/kernel.cu:191-200)
-    float pbf = fitness<Topo, MODE, POSREF>(cc, x, sh.rest, sh.tgt, nullptr);
+    float pbf = fitness<Topo, MODE, TERMS>(cc, x, sh.rest, sh.tgt, nullptr);
 
     // swarm argmin + unconditional first global-best copy (src/kernel.cu:297-304)
     int bidx;
@@ -116,7 +116,7 @@ __global__ void __launch_bounds__(kResidentMaxThreads<Topo::J>())
         for (int d = 0; d < D; ++d) x[d] = clamp_ref(x[d], sh.lo[d], sh.hi[d]);
 
         // updateLocalBests (src/kernel.cu:202-221): strict improvement
-        const float f = fitness<Topo, MODE, POSREF>(cc, x, sh.rest, sh.tgt, nullptr);
+        const float f = fitness<Topo, MODE, TERMS>(cc, x, sh.rest, sh.tgt, nullptr);
         if (f < pbf) {
             pbf = f;
 #pragma unroll
@@ -189,7 +189,7 @@ __global__ void __launch_bounds__(256) k_evaluate(const ChainConsts<Topo::J> cc,
 #pragma unroll
             for (int d = 0; d < D; ++d) tgt[d] = cc.tgt0[d];
         }
-        const float f = fitness<Topo, MODE, 2>(cc, x, rest, tgt, pos);
+        const float f = fitness<Topo, MODE, kTermRuntime>(cc, x, rest, tgt, pos);
         if (io.out_fitness) io.out_fitness[n] = f;
         if (io.out_positions) {
 #pragma unroll
@@ -204,13 +204,18 @@ static hipError_t run_resident(const ChainHost& ch, const SwarmIO& io, int block
 {
     const ChainConsts<Topo::J> cc = make_consts<Topo::J>(ch);
     const dim3 grid((unsigned)io.num_swarms), threads(block);
+    // Specialised topologies compile the optional terms in only when used; the
+    // generic ones test runtime flags.
     if constexpr (Topo::kGeneric) {
-        hipLaunchKernelGGL((k_swarm_resident<Topo, MODE, 2>), grid, threads, 0, stream, cc, io);
+        hipLaunchKernelGGL((k_swarm_resident<Topo, MODE, kTermRuntime>), grid, threads, 0, stream, cc, io);
     } else {
-        if (ch.use_posref)
-            hipLaunchKernelGGL((k_swarm_resident<Topo, MODE, 1>), grid, threads, 0, stream, cc, io);
-        else
-            hipLaunchKernelGGL((k_swarm_resident<Topo, MODE, 0>), grid, threads, 0, stream, cc, io);
+        const int terms = (ch.use_posref ? kTermPosRef : 0) | (ch.use_penalty ? kTermPenalty : 0);
+        switch (terms) {
+        case 0: hipLaunchKernelGGL((k_swarm_resident<Topo, MODE, 0>), grid, threads, 0, stream, cc, io); break;
+        case 1: hipLaunchKernelGGL((k_swarm_resident<Topo, MODE, 1>), grid, threads, 0, stream, cc, io); break;
+        case 2: hipLaunchKernelGGL((k_swarm_resident<Topo, MODE, 2>), grid, threads, 0, stream, cc, io); break;
+        default: hipLaunchKernelGGL((k_swarm_resident<Topo, MODE, 3>), grid, threads, 0, stream, cc, io); break;
+        }
     }
     return hipGetLastError();
 }

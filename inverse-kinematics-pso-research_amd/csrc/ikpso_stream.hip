@@ -58,11 +58,10 @@ __device__ __forceinline__ uint32_t stream_resolve_gbest(const StreamIO& io, int
 }
 
 // Chunk argmin of the local-best keys -> partial slot t&1; the winner lane
-// publishes its pbest vector (x if it improved in this launch, else from HBM).
+// publishes its pbest vector (its own stores of this launch, read back).
 template <int J>
 __device__ __forceinline__ void stream_publish_chunk(const StreamIO& io, int64_t b, int c, SwarmShared<J>& sh,
-                                                     uint32_t key, bool improved_now, const float* x,
-                                                     const float* pb_plane, int i)
+                                                     uint32_t key, const Planes& pl)
 {
     constexpr int D = 3 * J;
     int widx;
@@ -76,11 +75,11 @@ __device__ __forceinline__ void stream_publish_chunk(const StreamIO& io, int64_t
     if (threadIdx.x == widx) {
         float* dst = io.pvec + slot * D;
 #pragma unroll
-        for (int d = 0; d < D; ++d) dst[d] = improved_now ? x[d] : pb_plane[(int64_t)d * io.P + i];
+        for (int d = 0; d < D; ++d) dst[d] = pl.ld(2, d);
     }
 }
 
-template <class Topo, int MODE, int POSREF>
+template <class Topo, int MODE, int TERMS>
 __global__ void __launch_bounds__(kStreamChunk) k_stream_init(const ChainConsts<Topo::J> cc, const StreamIO io)
 {
     constexpr int J = Topo::J;
@@ -94,9 +93,7 @@ __global__ void __launch_bounds__(kStreamChunk) k_stream_init(const ChainConsts<
     stage_swarm_inputs<J>(cc, io.targets, io.start_pose, b, sh);
     __syncthreads();
 
-    float* X = io.state + b * 3 * D * P;
-    float* V = X + D * P;
-    float* PB = X + 2 * D * P;
+    const Planes pl(io.state + b * 3 * D * P, D, (int)P, i);
     float x[D];
     float pbf = 0.0f;
     if (active) {
@@ -106,11 +103,11 @@ __global__ void __launch_bounds__(kStreamChunk) k_stream_init(const ChainConsts<
 #pragma unroll
         for (int d = 0; d < D; ++d) {
             x[d] = sh.rest[d];
-            X[d * P + i] = x[d];
-            V[d * P + i] = __builtin_fmaf(rng.uniform(), 2.0f, -1.0f);
-            PB[d * P + i] = x[d];
+            pl.st(0, d, x[d]);
+            pl.st(1, d, __builtin_fmaf(rng.uniform(), 2.0f, -1.0f));
+            pl.st(2, d, x[d]);
         }
-        pbf = fitness<Topo, MODE, POSREF>(cc, x, sh.rest, sh.tgt, nullptr);
+        pbf = fitness<Topo, MODE, TERMS>(cc, x, sh.rest, sh.tgt, nullptr);
         io.pbf[b * P + i] = pbf;
         const int64_t n = io.num_swarms * P, k = b * P + i;
         io.rng[0 * n + k] = rng.d;
@@ -120,11 +117,11 @@ __global__ void __launch_bounds__(kStreamChunk) k_stream_init(const ChainConsts<
         io.rng[4 * n + k] = rng.v3;
         io.rng[5 * n + k] = rng.v4;
     }
-    stream_publish_chunk<J>(io, b, c, sh, active ? ordered_key(pbf) : 0xFFFFFFFFu, true, x, PB, i);
+    stream_publish_chunk<J>(io, b, c, sh, active ? ordered_key(pbf) : 0xFFFFFFFFu, pl);
     if (c == 0 && threadIdx.x == 0) io.gkey[(int64_t)(io.t & 1) * io.num_swarms + b] = 0xFFFFFFFFu;
 }
 
-template <class Topo, int MODE, int POSREF>
+template <class Topo, int MODE, int TERMS>
 __global__ void __launch_bounds__(kStreamChunk) k_stream_step(const ChainConsts<Topo::J> cc, const StreamIO io)
 {
     constexpr int J = Topo::J;
@@ -139,12 +136,8 @@ __global__ void __launch_bounds__(kStreamChunk) k_stream_step(const ChainConsts<
     stream_resolve_gbest<J>(io, b, c, sh);
     __syncthreads();
 
-    float* X = io.state + b * 3 * D * P;
-    float* V = X + D * P;
-    float* PB = X + 2 * D * P;
-    float x[D];
+    const Planes pl(io.state + b * 3 * D * P, D, (int)P, i);
     float pbf = 0.0f;
-    bool improved = false;
     if (active) {
         const int64_t n = io.num_swarms * P, k = b * P + i;
         Xorwow rng;
@@ -155,29 +148,61 @@ __global__ void __launch_bounds__(kStreamChunk) k_stream_step(const ChainConsts<
         rng.v3 = io.rng[4 * n + k];
         rng.v4 = io.rng[5 * n + k];
         pbf = io.pbf[b * P + i];
-#pragma unroll
-        for (int d = 0; d < D; ++d) x[d] = X[d * P + i];
-        // simulateParticlesKernel (src/kernel.cu:153-189)
+        // One node at a time: update its three angles (simulateParticlesKernel,
+        // src/kernel.cu:153-189: draws r1, r2, r3 per dimension in dimension
+        // order, then the clamp), store them, and fold the node into the
+        // fitness (calculateDistance, src/kernel.cu:64-151).  A node's FK needs
+        // only its own and its ancestors' angles, so this is the reference's
+        // update-all-then-evaluate with the same values and accumulation order,
+        // while only a handful of angles are live at a time.
         const float w = cc.w, c1 = cc.c1, c2 = cc.c2;
+        FitnessAcc<Topo, MODE, TERMS> acc(cc);
+        // Loads are software-pipelined one node ahead and every node ends in a
+        // scheduling barrier: left alone, the compiler hoists all 9J loads to
+        // the top (256 VGPRs, one wave per SIMD, latency-bound).
+        float nx[3], nv[3], npb[3];
 #pragma unroll
-        for (int d = 0; d < D; ++d) {
-            float v = V[d * P + i];
-            pso_update<MODE>(x[d], v, PB[d * P + i], sh.g[d], w, c1, c2, rng);
-            V[d * P + i] = v;
+        for (int ax = 0; ax < 3; ++ax) {
+            nx[ax] = pl.ld(0, ax);
+            nv[ax] = pl.ld(1, ax);
+            npb[ax] = pl.ld(2, ax);
         }
 #pragma unroll
-        for (int d = 0; d < D; ++d) {
-            x[d] = clamp_ref(x[d], sh.lo[d], sh.hi[d]);
-            X[d * P + i] = x[d];
+        for (int kn = 1; kn <= J; ++kn) {
+            float cx[3], cv[3], cpb[3];
+#pragma unroll
+            for (int ax = 0; ax < 3; ++ax) {
+                cx[ax] = nx[ax];
+                cv[ax] = nv[ax];
+                cpb[ax] = npb[ax];
+            }
+            if (kn < J) {
+#pragma unroll
+                for (int ax = 0; ax < 3; ++ax) {
+                    const int d = 3 * kn + ax;
+                    nx[ax] = pl.ld(0, d);
+                    nv[ax] = pl.ld(1, d);
+                    npb[ax] = pl.ld(2, d);
+                }
+            }
+#pragma unroll
+            for (int ax = 0; ax < 3; ++ax) {
+                const int d = 3 * (kn - 1) + ax;
+                pso_update<MODE>(cx[ax], cv[ax], cpb[ax], sh.g[d], w, c1, c2, rng);
+                pl.st(1, d, cv[ax]);
+                cx[ax] = clamp_ref(cx[ax], sh.lo[d], sh.hi[d]);
+                pl.st(0, d, cx[ax]);
+            }
+            acc.node(cc, kn, cx[0], cx[1], cx[2], sh.rest, sh.tgt, nullptr);
+            __builtin_amdgcn_sched_barrier(0);
         }
         // updateLocalBests (src/kernel.cu:202-221)
-        const float f = fitness<Topo, MODE, POSREF>(cc, x, sh.rest, sh.tgt, nullptr);
+        const float f = acc.finish(cc);
         if (f < pbf) {
-            improved = true;
             pbf = f;
             io.pbf[b * P + i] = f;
 #pragma unroll
-            for (int d = 0; d < D; ++d) PB[d * P + i] = x[d];
+            for (int d = 0; d < D; ++d) pl.st(2, d, pl.ld(0, d));  // this lane's own stores
         }
         io.rng[0 * n + k] = rng.d;
         io.rng[1 * n + k] = rng.v0;
@@ -186,7 +211,7 @@ __global__ void __launch_bounds__(kStreamChunk) k_stream_step(const ChainConsts<
         io.rng[4 * n + k] = rng.v3;
         io.rng[5 * n + k] = rng.v4;
     }
-    stream_publish_chunk<J>(io, b, c, sh, active ? ordered_key(pbf) : 0xFFFFFFFFu, improved, x, PB, i);
+    stream_publish_chunk<J>(io, b, c, sh, active ? ordered_key(pbf) : 0xFFFFFFFFu, pl);
 }
 
 template <class Topo, int MODE>
@@ -227,16 +252,16 @@ __global__ void __launch_bounds__(kStreamChunk) k_stream_finalize(const ChainCon
     }
 }
 
-template <class Topo, int MODE, int POSREF>
+template <class Topo, int MODE, int TERMS>
 static hipError_t run_stream(const ChainHost& ch, StreamIO io, int iterations, hipStream_t stream)
 {
     const ChainConsts<Topo::J> cc = make_consts<Topo::J>(ch);
     const dim3 grid((unsigned)(io.num_swarms * io.C)), threads(kStreamChunk);
     io.t = 0;
-    hipLaunchKernelGGL((k_stream_init<Topo, MODE, POSREF>), grid, threads, 0, stream, cc, io);
+    hipLaunchKernelGGL((k_stream_init<Topo, MODE, TERMS>), grid, threads, 0, stream, cc, io);
     for (int t = 1; t <= iterations; ++t) {
         io.t = t;
-        hipLaunchKernelGGL((k_stream_step<Topo, MODE, POSREF>), grid, threads, 0, stream, cc, io);
+        hipLaunchKernelGGL((k_stream_step<Topo, MODE, TERMS>), grid, threads, 0, stream, cc, io);
     }
     io.t = iterations + 1;
     hipLaunchKernelGGL((k_stream_finalize<Topo, MODE>), grid, threads, 0, stream, cc, io);
@@ -244,13 +269,18 @@ static hipError_t run_stream(const ChainHost& ch, StreamIO io, int iterations, h
 }
 
 template <class Topo, int MODE>
-static hipError_t run_stream_posref(const ChainHost& ch, const StreamIO& io, int iterations, hipStream_t stream)
+static hipError_t run_stream_terms(const ChainHost& ch, const StreamIO& io, int iterations, hipStream_t stream)
 {
-    if constexpr (Topo::kGeneric)
-        return run_stream<Topo, MODE, 2>(ch, io, iterations, stream);
-    else
-        return ch.use_posref ? run_stream<Topo, MODE, 1>(ch, io, iterations, stream)
-                             : run_stream<Topo, MODE, 0>(ch, io, iterations, stream);
+    if constexpr (Topo::kGeneric) {
+        return run_stream<Topo, MODE, kTermRuntime>(ch, io, iterations, stream);
+    } else {
+        switch ((ch.use_posref ? kTermPosRef : 0) | (ch.use_penalty ? kTermPenalty : 0)) {
+        case 0: return run_stream<Topo, MODE, 0>(ch, io, iterations, stream);
+        case 1: return run_stream<Topo, MODE, 1>(ch, io, iterations, stream);
+        case 2: return run_stream<Topo, MODE, 2>(ch, io, iterations, stream);
+        default: return run_stream<Topo, MODE, 3>(ch, io, iterations, stream);
+        }
+    }
 }
 
 hipError_t launch_stream(const ChainHost& ch, int mode, const StreamIO& io, int iterations, hipStream_t stream)
@@ -261,9 +291,9 @@ hipError_t launch_stream(const ChainHost& ch, int mode, const StreamIO& io, int 
     const bool ok = visit_topology(ch, [&](auto topo) {
         using T = decltype(topo);
         if (mode == IKPSO_ARITH_REFERENCE)
-            err = run_stream_posref<T, IKPSO_ARITH_REFERENCE>(ch, io, iterations, stream);
+            err = run_stream_terms<T, IKPSO_ARITH_REFERENCE>(ch, io, iterations, stream);
         else
-            err = run_stream_posref<T, IKPSO_ARITH_FAST>(ch, io, iterations, stream);
+            err = run_stream_terms<T, IKPSO_ARITH_FAST>(ch, io, iterations, stream);
     });
     return ok ? err : hipErrorInvalidValue;
 }

@@ -64,6 +64,34 @@ __device__ __forceinline__ void stage_swarm_inputs(const ChainConsts<J>& cc, con
 
 __device__ __forceinline__ void compiler_fence() { asm volatile("" ::: "memory"); }
 
+// One swarm's particle planes [3][D][P] (position | velocity | local best)
+// through a buffer resource: the lane's offset lives in one VGPR and the
+// per-dimension offset (plane*D + d) * P * 4 in an SGPR, instead of a 64-bit
+// VGPR address per access (which the compiler otherwise precomputes and keeps
+// live for every one of the 3D accesses).
+struct Planes {
+    __amdgpu_buffer_rsrc_t rsrc;
+    uint32_t p4;    // P * 4
+    uint32_t voff;  // lane * 4
+    int D;
+
+    __device__ __forceinline__ Planes(float* swarm_base, int D_, int P, int i)
+        : rsrc(__builtin_amdgcn_make_buffer_rsrc(swarm_base, 0, 3 * D_ * P * 4, 0x00020000)),
+          p4((uint32_t)P * 4u), voff((uint32_t)i * 4u), D(D_)
+    {
+    }
+    __device__ __forceinline__ float ld(int plane, int d) const
+    {
+        return __uint_as_float(
+            __builtin_amdgcn_raw_buffer_load_b32(rsrc, (int)voff, (int)((uint32_t)(plane * D + d) * p4), 0));
+    }
+    __device__ __forceinline__ void st(int plane, int d, float v) const
+    {
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rsrc, (int)voff,
+                                              (int)((uint32_t)(plane * D + d) * p4), 0);
+    }
+};
+
 // Swarm argmin of the local-best fitness keys, lowest particle index on ties
 // (thrust::min_element, src/kernel.cu:297,315).  One DPP wave min + ballot per
 // wave, a 16-entry LDS exchange, then every wave reduces the 16 entries
