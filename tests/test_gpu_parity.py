@@ -365,3 +365,31 @@ def test_config5_chain_with_penalty(oracle, device, arith):
     assert np.max(np.abs(fit - ofit) / ofit) < 1e-4
     assert np.max(np.abs(res - ores)) < 1e-3
     s.close()
+
+
+# ---------------------------------------------- per-frame driver (product)
+def test_frames_to_converge_matches_frames3(device, golden, tmp_path):
+    """The visualiser's recorded experiment (Documentation/Iteration_3, HEAD code):
+    20 test cases, N = 16384, 15 iterations per frame, converged when the sum of
+    effector distances <= 0.025, RNG carried across frames and cases.  Every case
+    is the same IK problem; only the generator stream differs, so the
+    distribution is compared with FRAMES_3 (two-sample KS, plus its envelope)."""
+    import json
+
+    from scipy.stats import ks_2samp
+
+    from ikpso.driver import LOG_FILES, FrameDriver
+
+    ref = json.load(open(golden / "frames3.json"))["frames"]
+    drv = FrameDriver(log_dir=str(tmp_path))
+    frames = drv.run_cases(20)
+    drv.close()
+    assert all(f > 0 for f in frames), frames
+    assert min(frames) >= 5 and 8 <= np.median(frames) <= 45, frames
+    assert ks_2samp(frames, ref).pvalue > 0.01, (frames, ref)
+    # the diagnostics logs have the reference's shape
+    lines = {n: open(tmp_path / n).read().splitlines() for n in LOG_FILES}
+    assert [int(x) for x in lines["IK-diagnostics-frames.txt"]] == frames
+    assert len(lines["IK-diagnostics-degrees.txt"]) == sum(frames)
+    assert all(l.count(";") == 21 for l in lines["IK-diagnostics-positions.txt"])
+    print("frames to converge:", frames, "median", np.median(frames), "mean", np.mean(frames))
