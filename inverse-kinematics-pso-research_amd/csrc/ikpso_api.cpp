@@ -100,6 +100,13 @@ M4 origin_matrix(const ikpso_node& n)
     return m4_mul(m, rz);
 }
 
+uint32_t as_bits(float f)
+{
+    uint32_t u;
+    memcpy(&u, &f, 4);
+    return u;
+}
+
 // Copy `bytes` from host, managed or device memory into host memory.
 ikpso_status fetch_any(void* dst, const void* src, size_t bytes)
 {
@@ -155,6 +162,14 @@ ikpso_status parse_chain(const std::vector<ikpso_node>& nodes, const ikpso_pso_c
         }
     }
     ch.E = E;
+#ifdef IKPSO_NO_UNIFORM_BOUNDS
+    ch.uniform_bounds = false;
+#else
+    ch.uniform_bounds = true;
+#endif
+    for (int d = 0; d < 3 * J && ch.uniform_bounds; ++d)
+        ch.uniform_bounds = ch.uniform_bounds && as_bits(ch.lo[d]) == as_bits(ch.lo[0]) &&
+                            as_bits(ch.hi[d]) == as_bits(ch.hi[0]);
     ref7 = ref7 && eff_mask == 0xE0ull;                // effectors = nodes 5, 6, 7
     serial = serial && eff_mask == (1ull << J);        // single tip effector
     ch.topo = ref7 ? TopoKind::Ref7 : (serial ? TopoKind::SerialTip : TopoKind::Generic);

@@ -87,6 +87,16 @@ struct Xorwow {
         return __builtin_fmaf((float)next(), 2.3283064e-10f, 1.16415322e-10f);
 #endif
     }
+    // c * uniform() with the scale folded in: fma(x, c*2^-32, c*2^-33).
+    __host__ __device__ __forceinline__ float scaled(float q, float h)
+    {
+#if IKPSO_ABL_NORNG
+        v4 += 0x9e3779b9u;
+        return __builtin_fmaf((float)v4, q, h);
+#else
+        return __builtin_fmaf((float)next(), q, h);
+#endif
+    }
 };
 
 __host__ __device__ inline void xorwow_seed(uint64_t seed, uint32_t st[6])
@@ -315,8 +325,11 @@ __device__ __forceinline__ Frame child_frame(const Frame& P, float a, float b, f
 // the resulting +0 leaves a finite sum unchanged bit for bit.
 // TERMS: which optional terms are compiled in -- kTermPosRef (distanceWeight
 // != 0: the positions[] term), kTermPenalty (soft joint limits), or
-// kTermRuntime (generic kernels: both decided by runtime flags).
-constexpr int kTermPosRef = 1, kTermPenalty = 2, kTermRuntime = 4;
+// kTermRuntime (generic kernels: both decided by runtime flags);
+// kTermUniformBounds: every angle has the same clamp bounds (the reference
+// scene: [0, 2pi] on every axis), read once from the kernarg into SGPRs
+// instead of per dimension from LDS.
+constexpr int kTermPosRef = 1, kTermPenalty = 2, kTermRuntime = 4, kTermUniformBounds = 8;
 
 template <class Topo, int MODE, int TERMS>
 struct FitnessAcc {
@@ -333,14 +346,15 @@ struct FitnessAcc {
         F[0] = origin_frame(cc.m0);
     }
 
-    // Node k (1..J) with its three Euler angles; nodes must come in index order.
+    // Node k (1..J) with its three Euler angles, its three rest angles and (for
+    // effectors) its target; nodes must come in index order.
     __device__ __forceinline__ void node(const ChainConsts<J>& cc, int k, float a, float b, float c,
-                                         const float* rest, const float* tgt, float* node_pos)
+                                         const float* rest3, const float* tgt3, float* node_pos)
     {
 #pragma clang fp contract(off)
         const int pk = Topo::kGeneric ? cc.parent[k] : Topo::parent(k);
         F[k] = child_frame<MODE>(F[pk], a, b, c, cc.len[k]);
-        const float dx = rest[3 * (k - 1) + 0] - a, dy = rest[3 * (k - 1) + 1] - b, dz = rest[3 * (k - 1) + 2] - c;
+        const float dx = rest3[0] - a, dy = rest3[1] - b, dz = rest3[2] - c;
         if constexpr (MODE == IKPSO_ARITH_REFERENCE) {
             rot_diff = rot_diff + ((dx * dx + dy * dy) + dz * dz);
         } else {
@@ -356,9 +370,9 @@ struct FitnessAcc {
             pos_diff += ((ex * ex + ey * ey) + ez * ez) + ew * ew;
         }
         if (Topo::effector(k)) {
-            const float ex = F[k].px - tgt[3 * (k - 1) + 0];
-            const float ey = F[k].py - tgt[3 * (k - 1) + 1];
-            const float ez = F[k].pz - tgt[3 * (k - 1) + 2];
+            const float ex = F[k].px - tgt3[0];
+            const float ey = F[k].py - tgt3[1];
+            const float ez = F[k].pz - tgt3[2];
             if constexpr (MODE == IKPSO_ARITH_REFERENCE) {
                 distance = distance + ((ex * ex + ey * ey) + ez * ez) * cc.eff_w[k];
             } else {
@@ -399,7 +413,8 @@ __device__ __forceinline__ float fitness(const ChainConsts<Topo::J>& cc, const f
     FitnessAcc<Topo, MODE, TERMS> acc(cc);
 #pragma unroll
     for (int k = 1; k <= Topo::J; ++k) {
-        acc.node(cc, k, x[3 * (k - 1) + 0], x[3 * (k - 1) + 1], x[3 * (k - 1) + 2], rest, tgt, node_pos);
+        acc.node(cc, k, x[3 * (k - 1) + 0], x[3 * (k - 1) + 1], x[3 * (k - 1) + 2], rest + 3 * (k - 1),
+                 tgt + 3 * (k - 1), node_pos);
 #if IKPSO_SCHED_NODE
         // One node at a time: keeps the scheduler from hoisting all 3J
         // independent sincos evaluations to the top of the evaluation.
@@ -433,22 +448,42 @@ __device__ __forceinline__ float residual(const ChainConsts<Topo::J>& cc, const 
 }
 
 // ------------------------------------------------------------ PSO update
+// PSO coefficients of one solve, uniform across the workgroup.
+struct PsoCoef {
+    float w, c1, c2;
+    float wq, c1q, c2q;  // c * 2^-32
+    float wh, c1h, c2h;  // c * 2^-33
+};
+
+template <class CC>
+__device__ __forceinline__ PsoCoef pso_coef(const CC& cc)
+{
+    return PsoCoef{cc.w, cc.c1, cc.c2, cc.wq, cc.c1q, cc.c2q, cc.wh, cc.c1h, cc.c2h};
+}
+
 // simulateParticlesKernel body for one dimension (src/kernel.cu:160-169):
 //   v = w*r1*v + c1*r2*(pb - x) + c2*r3*(g - x);  x += v
+// REFERENCE mode evaluates exactly that, unfused.  FAST mode folds each
+// coefficient into its uniform's affine map, c*r = c*(u*2^-32 + 2^-33) =
+// fma(u, c*2^-32, c*2^-33): one rounding where the reference has two (and
+// three fewer multiplies per dimension).
 template <int MODE>
-__device__ __forceinline__ void pso_update(float& x, float& v, float pb, float g, float w, float c1, float c2,
-                                           Xorwow& rng)
+__device__ __forceinline__ void pso_update(float& x, float& v, float pb, float g, const PsoCoef& k, Xorwow& rng)
 {
-    const float r1 = rng.uniform();
-    const float r2 = rng.uniform();
-    const float r3 = rng.uniform();
     if constexpr (MODE == IKPSO_ARITH_REFERENCE) {
+        const float r1 = rng.uniform();
+        const float r2 = rng.uniform();
+        const float r3 = rng.uniform();
+        {
 #pragma clang fp contract(off)
-        v = w * r1 * v + c1 * r2 * (pb - x) + c2 * r3 * (g - x);
-        x += v;
+            v = k.w * r1 * v + k.c1 * r2 * (pb - x) + k.c2 * r3 * (g - x);
+            x += v;
+        }
     } else {
-#pragma clang fp contract(fast)
-        v = w * r1 * v + c1 * r2 * (pb - x) + c2 * r3 * (g - x);
+        const float a = rng.scaled(k.wq, k.wh);
+        const float b = rng.scaled(k.c1q, k.c1h);
+        const float c = rng.scaled(k.c2q, k.c2h);
+        v = __builtin_fmaf(a, v, __builtin_fmaf(b, pb - x, c * (g - x)));
         x += v;
     }
 }

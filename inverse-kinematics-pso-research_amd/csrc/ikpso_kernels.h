@@ -29,6 +29,7 @@ struct ChainHost {
     float m0[12] = {};
     float w = 0, c1 = 0, c2 = 0, aw_j = 0, dw_j = 0, lim_w = 0;
     bool use_posref = false, use_penalty = false;
+    bool uniform_bounds = false;  // every angle has clamp bounds lo[0], hi[0]
 };
 
 // Evaluate-kernel parameters.
@@ -72,6 +73,12 @@ ChainConsts<J> make_consts(const ChainHost& h)
     c.w = h.w;
     c.c1 = h.c1;
     c.c2 = h.c2;
+    c.wq = h.w * 0x1p-32f;
+    c.c1q = h.c1 * 0x1p-32f;
+    c.c2q = h.c2 * 0x1p-32f;
+    c.wh = h.w * 0x1p-33f;
+    c.c1h = h.c1 * 0x1p-33f;
+    c.c2h = h.c2 * 0x1p-33f;
     c.aw_j = h.aw_j;
     c.dw_j = h.dw_j;
     c.lim_w = h.lim_w;

@@ -98,25 +98,64 @@ __global__ void __launch_bounds__(kResidentMaxThreads<Topo::J>())
     // swarm argmin + unconditional first global-best copy (src/kernel.cu:297-304)
     int bidx;
     uint32_t gkey = swarm_argmin<J>(sh, 0, active ? ordered_key(pbf) : 0xFFFFFFFFu, &bidx);
-    if (tid < D) sh.g[tid] = s_pb[tid * BLOCK + bidx];
+    copy_gbest<J, BLOCK>(sh, s_pb, bidx);
     __syncthreads();
 
-    const float w = cc.w, c1 = cc.c1, c2 = cc.c2;
+    const PsoCoef coef = pso_coef(cc);
     for (int it = 0; it < io.iterations; ++it) {
         compiler_fence();
-        // simulateParticlesKernel (src/kernel.cu:153-189)
+        // simulateParticlesKernel (src/kernel.cu:153-189) + calculateDistance
+        // (src/kernel.cu:64-151), one node at a time: the node's three angles
+        // are updated (r1, r2, r3 per dimension, in dimension order) and
+        // clamped, then the node is folded into the FK/fitness.  A node's FK
+        // needs only its own and its ancestors' angles, so this computes the
+        // reference's update-all-then-evaluate values in the same order.  The
+        // node's LDS operands (local best, global best, rest pose, target) are
+        // loaded one node ahead so their latency hides under the previous node.
+        FitnessAcc<Topo, MODE, TERMS> acc(cc);
+        float npb[3], ng[3], nrest[3], ntgt[3];
 #pragma unroll
-        for (int d = 0; d < D; ++d) {
-            pso_update<MODE>(x[d], v[d], s_pb[d * BLOCK + tid], sh.g[d], w, c1, c2, rng);
-#if IKPSO_SCHED_DIM
-            if (d % 3 == 2) __builtin_amdgcn_sched_barrier(0);
-#endif
+        for (int ax = 0; ax < 3; ++ax) {
+            npb[ax] = s_pb[ax * BLOCK + tid];
+            ng[ax] = sh.g[ax];
+            nrest[ax] = sh.rest[ax];
+            ntgt[ax] = Topo::effector(1) ? sh.tgt[ax] : 0.0f;
         }
 #pragma unroll
-        for (int d = 0; d < D; ++d) x[d] = clamp_ref(x[d], sh.lo[d], sh.hi[d]);
+        for (int k = 1; k <= J; ++k) {
+            float cpb[3], cg[3], crest[3], ctgt[3];
+#pragma unroll
+            for (int ax = 0; ax < 3; ++ax) {
+                cpb[ax] = npb[ax];
+                cg[ax] = ng[ax];
+                crest[ax] = nrest[ax];
+                ctgt[ax] = ntgt[ax];
+            }
+            if (k < J) {
+#pragma unroll
+                for (int ax = 0; ax < 3; ++ax) {
+                    const int d = 3 * k + ax;
+                    npb[ax] = s_pb[d * BLOCK + tid];
+                    ng[ax] = sh.g[d];
+                    nrest[ax] = sh.rest[d];
+                    ntgt[ax] = Topo::effector(k + 1) ? sh.tgt[d] : 0.0f;
+                }
+            }
+#pragma unroll
+            for (int ax = 0; ax < 3; ++ax) {
+                const int d = 3 * (k - 1) + ax;
+                pso_update<MODE>(x[d], v[d], cpb[ax], cg[ax], coef, rng);
+                if constexpr (TERMS & kTermUniformBounds)
+                    x[d] = clamp_ref(x[d], cc.lo[0], cc.hi[0]);
+                else
+                    x[d] = clamp_ref(x[d], sh.lo[d], sh.hi[d]);
+            }
+            acc.node(cc, k, x[3 * (k - 1)], x[3 * (k - 1) + 1], x[3 * (k - 1) + 2], crest, ctgt, nullptr);
+            __builtin_amdgcn_sched_barrier(0);
+        }
 
         // updateLocalBests (src/kernel.cu:202-221): strict improvement
-        const float f = fitness<Topo, MODE, TERMS>(cc, x, sh.rest, sh.tgt, nullptr);
+        const float f = acc.finish(cc);
         if (f < pbf) {
             pbf = f;
 #pragma unroll
@@ -132,7 +171,7 @@ __global__ void __launch_bounds__(kResidentMaxThreads<Topo::J>())
 #endif
         if (bmin < gkey) {  // uniform across the workgroup
             gkey = bmin;
-            if (tid < D) sh.g[tid] = s_pb[tid * BLOCK + bidx];
+            copy_gbest<J, BLOCK>(sh, s_pb, bidx);
             __syncthreads();
         }
     }
@@ -209,9 +248,24 @@ static hipError_t run_resident(const ChainHost& ch, const SwarmIO& io, int block
     if constexpr (Topo::kGeneric) {
         hipLaunchKernelGGL((k_swarm_resident<Topo, MODE, kTermRuntime>), grid, threads, 0, stream, cc, io);
     } else {
-        const int terms = (ch.use_posref ? kTermPosRef : 0) | (ch.use_penalty ? kTermPenalty : 0);
+        const int terms = (ch.use_posref ? kTermPosRef : 0) | (ch.use_penalty ? kTermPenalty : 0) |
+                          (ch.uniform_bounds ? kTermUniformBounds : 0);
         switch (terms) {
-        case 0: hipLaunchKernelGGL((k_swarm_resident<Topo, MODE, 0>), grid, threads, 0, stream, cc, io); break;
+        case kTermUniformBounds:
+            hipLaunchKernelGGL((k_swarm_resident<Topo, MODE, kTermUniformBounds>), grid, threads, 0, stream, cc, io);
+            break;
+        case kTermUniformBounds | kTermPenalty:
+            hipLaunchKernelGGL((k_swarm_resident<Topo, MODE, kTermUniformBounds | kTermPenalty>), grid, threads, 0,
+                               stream, cc, io);
+            break;
+        case 0:
+        case kTermUniformBounds | kTermPosRef:
+            if (terms) {  // uniform bounds + distance term: the per-dimension path
+                hipLaunchKernelGGL((k_swarm_resident<Topo, MODE, 1>), grid, threads, 0, stream, cc, io);
+                break;
+            }
+            hipLaunchKernelGGL((k_swarm_resident<Topo, MODE, 0>), grid, threads, 0, stream, cc, io);
+            break;
         case 1: hipLaunchKernelGGL((k_swarm_resident<Topo, MODE, 1>), grid, threads, 0, stream, cc, io); break;
         case 2: hipLaunchKernelGGL((k_swarm_resident<Topo, MODE, 2>), grid, threads, 0, stream, cc, io); break;
         default: hipLaunchKernelGGL((k_swarm_resident<Topo, MODE, 3>), grid, threads, 0, stream, cc, io); break;

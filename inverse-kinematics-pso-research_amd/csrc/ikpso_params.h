@@ -28,6 +28,8 @@ struct ChainConsts {
     // aux = [posref 4J | soft_lo 3J | soft_hi 3J].
     const float* aux;
     float w, c1, c2;          // inertia, local, global
+    float wq, c1q, c2q;       // the same times 2^-32 (exact): FAST mode folds
+    float wh, c1h, c2h;       // the uniform's affine map, times 2^-33 (exact)
     float aw_j, dw_j, lim_w;  // angleWeight/J, distanceWeight/J, limit weight
     int32_t use_posref, use_penalty;
     int32_t num_eff;

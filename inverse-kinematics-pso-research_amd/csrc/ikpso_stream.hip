@@ -155,7 +155,7 @@ __global__ void __launch_bounds__(kStreamChunk) k_stream_step(const ChainConsts<
         // only its own and its ancestors' angles, so this is the reference's
         // update-all-then-evaluate with the same values and accumulation order,
         // while only a handful of angles are live at a time.
-        const float w = cc.w, c1 = cc.c1, c2 = cc.c2;
+        const PsoCoef coef = pso_coef(cc);
         FitnessAcc<Topo, MODE, TERMS> acc(cc);
         // Loads are software-pipelined one node ahead and every node ends in a
         // scheduling barrier: left alone, the compiler hoists all 9J loads to
@@ -188,12 +188,15 @@ __global__ void __launch_bounds__(kStreamChunk) k_stream_step(const ChainConsts<
 #pragma unroll
             for (int ax = 0; ax < 3; ++ax) {
                 const int d = 3 * (kn - 1) + ax;
-                pso_update<MODE>(cx[ax], cv[ax], cpb[ax], sh.g[d], w, c1, c2, rng);
+                pso_update<MODE>(cx[ax], cv[ax], cpb[ax], sh.g[d], coef, rng);
                 pl.st(1, d, cv[ax]);
-                cx[ax] = clamp_ref(cx[ax], sh.lo[d], sh.hi[d]);
+                if constexpr (TERMS & kTermUniformBounds)
+                    cx[ax] = clamp_ref(cx[ax], cc.lo[0], cc.hi[0]);
+                else
+                    cx[ax] = clamp_ref(cx[ax], sh.lo[d], sh.hi[d]);
                 pl.st(0, d, cx[ax]);
             }
-            acc.node(cc, kn, cx[0], cx[1], cx[2], sh.rest, sh.tgt, nullptr);
+            acc.node(cc, kn, cx[0], cx[1], cx[2], sh.rest + 3 * (kn - 1), sh.tgt + 3 * (kn - 1), nullptr);
             __builtin_amdgcn_sched_barrier(0);
         }
         // updateLocalBests (src/kernel.cu:202-221)
@@ -274,7 +277,14 @@ static hipError_t run_stream_terms(const ChainHost& ch, const StreamIO& io, int 
     if constexpr (Topo::kGeneric) {
         return run_stream<Topo, MODE, kTermRuntime>(ch, io, iterations, stream);
     } else {
-        switch ((ch.use_posref ? kTermPosRef : 0) | (ch.use_penalty ? kTermPenalty : 0)) {
+        switch ((ch.use_posref ? kTermPosRef : 0) | (ch.use_penalty ? kTermPenalty : 0) |
+                (ch.uniform_bounds ? kTermUniformBounds : 0)) {
+        case kTermUniformBounds: return run_stream<Topo, MODE, kTermUniformBounds>(ch, io, iterations, stream);
+        case kTermUniformBounds | kTermPenalty:
+            return run_stream<Topo, MODE, kTermUniformBounds | kTermPenalty>(ch, io, iterations, stream);
+        case kTermUniformBounds | kTermPosRef: return run_stream<Topo, MODE, 1>(ch, io, iterations, stream);
+        case kTermUniformBounds | kTermPosRef | kTermPenalty:
+            return run_stream<Topo, MODE, 3>(ch, io, iterations, stream);
         case 0: return run_stream<Topo, MODE, 0>(ch, io, iterations, stream);
         case 1: return run_stream<Topo, MODE, 1>(ch, io, iterations, stream);
         case 2: return run_stream<Topo, MODE, 2>(ch, io, iterations, stream);

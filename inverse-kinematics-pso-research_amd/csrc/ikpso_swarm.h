@@ -95,22 +95,52 @@ struct Planes {
 // Swarm argmin of the local-best fitness keys, lowest particle index on ties
 // (thrust::min_element, src/kernel.cu:297,315).  One DPP wave min + ballot per
 // wave, a 16-entry LDS exchange, then every wave reduces the 16 entries
-// redundantly, so the result is uniform without a second barrier.
+// redundantly, so the result is uniform without a second barrier.  Everything
+// after the wave min is scalar (wave id, first lane, winner index): the only
+// per-lane value is the lane id from mbcnt, so nothing here needs threadIdx
+// kept live across the loop (the compiler spilled it, and the reload sat on
+// the barrier's critical path).
+__device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
+
+// Lane id recomputed at the point of use (two VALU ops): an opaque asm, so the
+// compiler can neither hoist it out of the iteration loop nor keep it live
+// (and spill it) across the loop body.
+__device__ __forceinline__ int lane_id_here()
+{
+    int lane;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
+    return lane;
+}
+
 template <int J>
 __device__ __forceinline__ uint32_t swarm_argmin(SwarmShared<J>& sh, int par, uint32_t key, int* out_idx)
 {
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int lane = lane_id_here(), wave = wave_id();
     const int nwaves = blockDim.x >> 6;
     const uint32_t wmin = wave_min_u32(key);
-    if (lane == wave_first_lane_eq(key, wmin)) {
+    const int first = wave_first_lane_eq(key, wmin);
+    if (lane == 0) {
         sh.key[par][wave] = wmin;
-        sh.idx[par][wave] = tid;
+        sh.idx[par][wave] = wave * 64 + first;
     }
     __syncthreads();
     const uint32_t k2 = lane < nwaves ? sh.key[par][lane] : 0xFFFFFFFFu;
     const uint32_t bmin = wave_min_u32(k2);
-    *out_idx = sh.idx[par][wave_first_lane_eq(k2, bmin)];
+    *out_idx = __builtin_amdgcn_readfirstlane(sh.idx[par][wave_first_lane_eq(k2, bmin)]);
     return bmin;
+}
+
+// sh.g = local best of particle `idx` (updateGlobalBestCoordsKernel,
+// src/kernel.cu:268-277), copied by the first wave; the caller barriers.
+template <int J, int BLOCK>
+__device__ __forceinline__ void copy_gbest(SwarmShared<J>& sh, const float* s_pb, int idx)
+{
+    constexpr int D = 3 * J;
+    static_assert(D <= 64, "one wave copies the global best");
+    if (wave_id() == 0) {
+        const int lane = lane_id_here();
+        if (lane < D) sh.g[lane] = s_pb[lane * BLOCK + idx];
+    }
 }
 
 // Visit the kernel instantiation for (topology, J, mode).  Returns false when
