@@ -1,0 +1,18 @@
+// ikpso_inst_generic_a.hip -- kernel instantiations (generated layout: one unit per
+// heavy (topology, mode[, family]) so the build parallelises).
+#include "ikpso_topo_impl.h"
+
+namespace ikpso {
+#ifndef IKPSO_EXPERIMENT_REF7_ONLY
+template struct ModeOps<TopoGeneric<1>, IKPSO_ARITH_FAST>;
+template struct ModeOps<TopoGeneric<1>, IKPSO_ARITH_REFERENCE>;
+template struct ModeOps<TopoGeneric<2>, IKPSO_ARITH_FAST>;
+template struct ModeOps<TopoGeneric<2>, IKPSO_ARITH_REFERENCE>;
+template struct ModeOps<TopoGeneric<3>, IKPSO_ARITH_FAST>;
+template struct ModeOps<TopoGeneric<3>, IKPSO_ARITH_REFERENCE>;
+template struct ModeOps<TopoGeneric<4>, IKPSO_ARITH_FAST>;
+template struct ModeOps<TopoGeneric<4>, IKPSO_ARITH_REFERENCE>;
+template struct ModeOps<TopoGeneric<5>, IKPSO_ARITH_FAST>;
+template struct ModeOps<TopoGeneric<5>, IKPSO_ARITH_REFERENCE>;
+#endif
+}  // namespace ikpso

@@ -1,0 +1,7 @@
+// ikpso_inst_ref7_fast.hip -- kernel instantiations (generated layout: one unit per
+// heavy (topology, mode[, family]) so the build parallelises).
+#include "ikpso_topo_impl.h"
+
+namespace ikpso {
+template struct ModeOps<TopoRef7, IKPSO_ARITH_FAST>;
+}  // namespace ikpso

@@ -1,0 +1,9 @@
+// ikpso_inst_serial20_evaluate_fast.hip -- kernel instantiations (generated layout: one unit per
+// heavy (topology, mode[, family]) so the build parallelises).
+#include "ikpso_topo_impl.h"
+
+namespace ikpso {
+#ifndef IKPSO_EXPERIMENT_REF7_ONLY
+template hipError_t ModeOps<TopoSerialTip<20>, IKPSO_ARITH_FAST>::evaluate(const ChainHost&, const EvalIO&, hipStream_t);
+#endif
+}  // namespace ikpso

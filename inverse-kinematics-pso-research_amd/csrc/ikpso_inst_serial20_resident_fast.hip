@@ -1,0 +1,9 @@
+// ikpso_inst_serial20_resident_fast.hip -- kernel instantiations (generated layout: one unit per
+// heavy (topology, mode[, family]) so the build parallelises).
+#include "ikpso_topo_impl.h"
+
+namespace ikpso {
+#ifndef IKPSO_EXPERIMENT_REF7_ONLY
+template hipError_t ModeOps<TopoSerialTip<20>, IKPSO_ARITH_FAST>::resident(const ChainHost&, const SwarmIO&, int, hipStream_t);
+#endif
+}  // namespace ikpso

@@ -1,0 +1,9 @@
+// ikpso_inst_serial20_stream_ref.hip -- kernel instantiations (generated layout: one unit per
+// heavy (topology, mode[, family]) so the build parallelises).
+#include "ikpso_topo_impl.h"
+
+namespace ikpso {
+#ifndef IKPSO_EXPERIMENT_REF7_ONLY
+template hipError_t ModeOps<TopoSerialTip<20>, IKPSO_ARITH_REFERENCE>::stream(const ChainHost&, const StreamIO&, int, hipStream_t);
+#endif
+}  // namespace ikpso

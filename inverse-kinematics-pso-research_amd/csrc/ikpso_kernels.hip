@@ -1,28 +1,22 @@
-// ikpso_kernels.hip -- gfx950 kernels of the PSO inverse-kinematics hot path.
+// ikpso_kernels.hip -- host-side dispatch of the gfx950 kernels of the PSO
+// inverse-kinematics hot path, and the generator-seeding kernel.
 //
 // Replaces the reference's per-iteration launch chain (src/kernel.cu:279-327:
 // initParticlesKernel, initLocalBests, thrust::min_element, a blocking D2H
 // copy and updateGlobalBestCoordsKernel per iteration) with ONE launch per
-// batch of swarms:
-//
-//   k_swarm_resident: one workgroup = one swarm, one lane = one particle
-//     (P <= 1024).  Position, velocity, local best, local-best fitness and the
-//     XORWOW state of a particle stay in VGPRs for all iterations; the chain
-//     constants sit in the kernarg segment (scalar loads); the swarm argmin is
-//     a DPP wave64 min + ballot, then one 16-entry LDS pass; the global-best
-//     vector is broadcast through LDS only when it strictly improves (the
-//     `globalMin > currentGlobalMin` test of src/kernel.cu:318).  HBM traffic
-//     is the RNG state in/out and the outputs: the kernel is VALU-bound.
+// batch of swarms (k_swarm_resident, ikpso_resident.h) or, for swarms larger
+// than a workgroup, one launch per iteration (ikpso_stream.h).  Each compiled
+// topology's kernels live in their own translation unit (ikpso_inst_*.hip);
+// this file routes a parsed chain to them.
 //
 //   k_init_generators: curand_init(seed_base + i, 0, 0) per state
 //     (randInitKernel, src/utility_kernels.cuh:21-31).
-//
-//   k_evaluate: FK + fitness of given angle vectors (parity/KAT entry).
 #include <hip/hip_runtime.h>
 
 #include "ikpso_device.h"
 #include "ikpso_kernels.h"
 #include "ikpso_swarm.h"
+#include "ikpso_topo_ops.h"
 
 namespace ikpso {
 
@@ -60,231 +54,6 @@ hipError_t launch_init_generators(ikpso_rng_state* st, int64_t count, uint64_t s
     return hipGetLastError();
 }
 
-// ------------------------------------------------------- resident swarm kernel
-template <class Topo, int MODE, int TERMS>
-__global__ void __launch_bounds__(kResidentMaxThreads<Topo::J>())
-    k_swarm_resident(const ChainConsts<Topo::J> cc, const SwarmIO io)
-{
-    constexpr int J = Topo::J;
-    constexpr int D = 3 * J;
-    constexpr int BLOCK = kResidentMaxThreads<J>();
-    const int64_t b = blockIdx.x;
-    const int tid = threadIdx.x;
-    const int P = io.P;
-    const bool active = tid < P;
-
-    __shared__ SwarmShared<J> sh;
-    // Local-best positions, [d][lane]: read once per iteration by the update,
-    // written on improvement; consecutive lanes hit consecutive banks.
-    __shared__ float s_pb[D * BLOCK];
-    stage_swarm_inputs<J>(cc, io.targets, io.start_pose, b, sh);
-
-    Xorwow rng{0, 0, 0, 0, 0, 0};
-    if (active) load_rng(rng, io.rng + b * P + tid);
-    __syncthreads();
-
-    // initParticlesKernel (src/kernel.cu:223-266): warm start at the current
-    // pose, v = U*2-1 (D draws in dimension order), pbest = x.
-    float x[D], v[D];
-#pragma unroll
-    for (int d = 0; d < D; ++d) {
-        x[d] = sh.rest[d];
-        v[d] = __builtin_fmaf(rng.uniform(), 2.0f, -1.0f);
-        s_pb[d * BLOCK + tid] = x[d];
-    }
-    // initLocalBests (src/kernel.cu:191-200)
-    float pbf = fitness<Topo, MODE, TERMS>(cc, x, sh.rest, sh.tgt, nullptr);
-
-    // swarm argmin + unconditional first global-best copy (src/kernel.cu:297-304)
-    int bidx;
-    uint32_t gkey = swarm_argmin<J>(sh, 0, active ? ordered_key(pbf) : 0xFFFFFFFFu, &bidx);
-    copy_gbest<J, BLOCK>(sh, s_pb, bidx);
-    __syncthreads();
-
-    const PsoCoef coef = pso_coef(cc);
-    for (int it = 0; it < io.iterations; ++it) {
-        compiler_fence();
-        // simulateParticlesKernel (src/kernel.cu:153-189) + calculateDistance
-        // (src/kernel.cu:64-151), one node at a time: the node's three angles
-        // are updated (r1, r2, r3 per dimension, in dimension order) and
-        // clamped, then the node is folded into the FK/fitness.  A node's FK
-        // needs only its own and its ancestors' angles, so this computes the
-        // reference's update-all-then-evaluate values in the same order.  The
-        // node's LDS operands (local best, global best, rest pose, target) are
-        // loaded one node ahead so their latency hides under the previous node.
-        FitnessAcc<Topo, MODE, TERMS> acc(cc);
-        float npb[3], ng[3], nrest[3], ntgt[3];
-#pragma unroll
-        for (int ax = 0; ax < 3; ++ax) {
-            npb[ax] = s_pb[ax * BLOCK + tid];
-            ng[ax] = sh.g[ax];
-            nrest[ax] = sh.rest[ax];
-            ntgt[ax] = Topo::effector(1) ? sh.tgt[ax] : 0.0f;
-        }
-#pragma unroll
-        for (int k = 1; k <= J; ++k) {
-            float cpb[3], cg[3], crest[3], ctgt[3];
-#pragma unroll
-            for (int ax = 0; ax < 3; ++ax) {
-                cpb[ax] = npb[ax];
-                cg[ax] = ng[ax];
-                crest[ax] = nrest[ax];
-                ctgt[ax] = ntgt[ax];
-            }
-            if (k < J) {
-#pragma unroll
-                for (int ax = 0; ax < 3; ++ax) {
-                    const int d = 3 * k + ax;
-                    npb[ax] = s_pb[d * BLOCK + tid];
-                    ng[ax] = sh.g[d];
-                    nrest[ax] = sh.rest[d];
-                    ntgt[ax] = Topo::effector(k + 1) ? sh.tgt[d] : 0.0f;
-                }
-            }
-#pragma unroll
-            for (int ax = 0; ax < 3; ++ax) {
-                const int d = 3 * (k - 1) + ax;
-                pso_update<MODE>(x[d], v[d], cpb[ax], cg[ax], coef, rng);
-                if constexpr (TERMS & kTermUniformBounds)
-                    x[d] = clamp_ref(x[d], cc.lo[0], cc.hi[0]);
-                else
-                    x[d] = clamp_ref(x[d], sh.lo[d], sh.hi[d]);
-            }
-            acc.node(cc, k, x[3 * (k - 1)], x[3 * (k - 1) + 1], x[3 * (k - 1) + 2], crest, ctgt, nullptr);
-            __builtin_amdgcn_sched_barrier(0);
-        }
-
-        // updateLocalBests (src/kernel.cu:202-221): strict improvement
-        const float f = acc.finish(cc);
-        if (f < pbf) {
-            pbf = f;
-#pragma unroll
-            for (int d = 0; d < D; ++d) s_pb[d * BLOCK + tid] = x[d];
-        }
-
-        // thrust::min_element + `globalMin > currentGlobalMin` (src/kernel.cu:315-323)
-#if IKPSO_ABL_NOSYNC  // timing-only ablation: no swarm argmin
-        const uint32_t bmin = gkey;
-        asm volatile("" ::"v"(pbf));
-#else
-        const uint32_t bmin = swarm_argmin<J>(sh, (it + 1) & 1, active ? ordered_key(pbf) : 0xFFFFFFFFu, &bidx);
-#endif
-        if (bmin < gkey) {  // uniform across the workgroup
-            gkey = bmin;
-            copy_gbest<J, BLOCK>(sh, s_pb, bidx);
-            __syncthreads();
-        }
-    }
-
-    // outputs: Coordinates result (updateGlobalBestCoordsKernel) + fitness + residual
-    compiler_fence();
-    if (tid < D) io.out_angles[b * D + tid] = sh.g[tid];
-    if (tid == 0 && io.out_fitness) io.out_fitness[b] = key_to_float(gkey);
-    if (io.out_residual && tid < 64) {
-        float g[D];
-#pragma unroll
-        for (int d = 0; d < D; ++d) g[d] = sh.g[d];
-        const float r = residual<Topo, MODE>(cc, g, sh.tgt);
-        if (tid == 0) io.out_residual[b] = r;
-    }
-    if (active) {
-        store_rng(rng, io.rng + b * P + tid);
-        if (io.dump_particles) {  // reference particles layout [3][D][P] per swarm
-            float* base = io.dump_particles + b * (int64_t)3 * D * P;
-#pragma unroll
-            for (int d = 0; d < D; ++d) {
-                base[(int64_t)d * P + tid] = x[d];
-                base[(int64_t)(D + d) * P + tid] = v[d];
-                base[(int64_t)(2 * D + d) * P + tid] = s_pb[d * BLOCK + tid];
-            }
-        }
-        if (io.dump_bests) io.dump_bests[b * P + tid] = pbf;
-    }
-}
-
-// ----------------------------------------------------------- evaluate kernel
-template <class Topo, int MODE>
-__global__ void __launch_bounds__(256) k_evaluate(const ChainConsts<Topo::J> cc, EvalIO io)
-{
-    constexpr int J = Topo::J;
-    constexpr int D = 3 * J;
-    for (int64_t n = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; n < io.n;
-         n += (int64_t)gridDim.x * blockDim.x) {
-        float x[D], rest[D], tgt[D], pos[D];
-#pragma unroll
-        for (int d = 0; d < D; ++d) {
-            x[d] = io.angles[n * D + d];
-            rest[d] = io.rest ? io.rest[n * D + d] : cc.rest[d];
-        }
-        if (io.targets) {
-#pragma unroll
-            for (int k = 1; k <= J; ++k) {
-                const int s = cc.eff_slot[k];
-#pragma unroll
-                for (int c = 0; c < 3; ++c)
-                    tgt[3 * (k - 1) + c] = s >= 0 ? io.targets[(n * cc.num_eff + s) * 3 + c] : 0.0f;
-            }
-        } else {
-#pragma unroll
-            for (int d = 0; d < D; ++d) tgt[d] = cc.tgt0[d];
-        }
-        const float f = fitness<Topo, MODE, kTermRuntime>(cc, x, rest, tgt, pos);
-        if (io.out_fitness) io.out_fitness[n] = f;
-        if (io.out_positions) {
-#pragma unroll
-            for (int d = 0; d < D; ++d) io.out_positions[n * D + d] = pos[d];
-        }
-    }
-}
-
-// --------------------------------------------------------------- dispatch
-template <class Topo, int MODE>
-static hipError_t run_resident(const ChainHost& ch, const SwarmIO& io, int block, hipStream_t stream)
-{
-    const ChainConsts<Topo::J> cc = make_consts<Topo::J>(ch);
-    const dim3 grid((unsigned)io.num_swarms), threads(block);
-    // Specialised topologies compile the optional terms in only when used; the
-    // generic ones test runtime flags.
-    if constexpr (Topo::kGeneric) {
-        hipLaunchKernelGGL((k_swarm_resident<Topo, MODE, kTermRuntime>), grid, threads, 0, stream, cc, io);
-    } else {
-        const int terms = (ch.use_posref ? kTermPosRef : 0) | (ch.use_penalty ? kTermPenalty : 0) |
-                          (ch.uniform_bounds ? kTermUniformBounds : 0);
-        switch (terms) {
-        case kTermUniformBounds:
-            hipLaunchKernelGGL((k_swarm_resident<Topo, MODE, kTermUniformBounds>), grid, threads, 0, stream, cc, io);
-            break;
-        case kTermUniformBounds | kTermPenalty:
-            hipLaunchKernelGGL((k_swarm_resident<Topo, MODE, kTermUniformBounds | kTermPenalty>), grid, threads, 0,
-                               stream, cc, io);
-            break;
-        case 0:
-        case kTermUniformBounds | kTermPosRef:
-            if (terms) {  // uniform bounds + distance term: the per-dimension path
-                hipLaunchKernelGGL((k_swarm_resident<Topo, MODE, 1>), grid, threads, 0, stream, cc, io);
-                break;
-            }
-            hipLaunchKernelGGL((k_swarm_resident<Topo, MODE, 0>), grid, threads, 0, stream, cc, io);
-            break;
-        case 1: hipLaunchKernelGGL((k_swarm_resident<Topo, MODE, 1>), grid, threads, 0, stream, cc, io); break;
-        case 2: hipLaunchKernelGGL((k_swarm_resident<Topo, MODE, 2>), grid, threads, 0, stream, cc, io); break;
-        default: hipLaunchKernelGGL((k_swarm_resident<Topo, MODE, 3>), grid, threads, 0, stream, cc, io); break;
-        }
-    }
-    return hipGetLastError();
-}
-
-template <class Topo, int MODE>
-static hipError_t run_evaluate(const ChainHost& ch, const EvalIO& io, hipStream_t stream)
-{
-    const ChainConsts<Topo::J> cc = make_consts<Topo::J>(ch);
-    int64_t blocks = (io.n + 255) / 256;
-    if (blocks > 8192) blocks = 8192;
-    if (blocks < 1) blocks = 1;
-    hipLaunchKernelGGL((k_evaluate<Topo, MODE>), dim3((unsigned)blocks), dim3(256), 0, stream, cc, io);
-    return hipGetLastError();
-}
-
 int resident_max_threads(const ChainHost& ch)
 {
     int r = 0;
@@ -315,10 +84,7 @@ hipError_t launch_resident(const ChainHost& ch, int mode, const SwarmIO& io, hip
     hipError_t err = hipErrorInvalidValue;
     const bool ok = visit_topology(ch, [&](auto topo) {
         using T = decltype(topo);
-        if (mode == IKPSO_ARITH_REFERENCE)
-            err = run_resident<T, IKPSO_ARITH_REFERENCE>(ch, io, block, stream);
-        else
-            err = run_resident<T, IKPSO_ARITH_FAST>(ch, io, block, stream);
+        err = TopoOps<T>::resident(ch, mode, io, block, stream);
     });
     return ok ? err : hipErrorInvalidValue;
 }
@@ -330,12 +96,37 @@ hipError_t launch_evaluate(const ChainHost& ch, int mode, const EvalIO& io, hipS
     hipError_t err = hipErrorInvalidValue;
     const bool ok = visit_topology(ch, [&](auto topo) {
         using T = decltype(topo);
-        if (mode == IKPSO_ARITH_REFERENCE)
-            err = run_evaluate<T, IKPSO_ARITH_REFERENCE>(ch, io, stream);
-        else
-            err = run_evaluate<T, IKPSO_ARITH_FAST>(ch, io, stream);
+        err = TopoOps<T>::evaluate(ch, mode, io, stream);
     });
     return ok ? err : hipErrorInvalidValue;
 }
+
+hipError_t launch_stream(const ChainHost& ch, int mode, const StreamIO& io, int iterations, hipStream_t stream)
+{
+    if (io.num_swarms <= 0) return hipSuccess;
+    if (!ch.aux_dev || io.C != (io.P + kStreamChunk - 1) / kStreamChunk) return hipErrorInvalidValue;
+    hipError_t err = hipErrorInvalidValue;
+    const bool ok = visit_topology(ch, [&](auto topo) {
+        using T = decltype(topo);
+        err = TopoOps<T>::stream(ch, mode, io, iterations, stream);
+    });
+    return ok ? err : hipErrorInvalidValue;
+}
+
+// Workspace bytes for B swarms of P particles and D angles (state excluded when
+// the caller provides it).
+size_t stream_workspace_bytes(int64_t B, int P, int D, bool with_state)
+{
+    const int64_t C = (P + kStreamChunk - 1) / kStreamChunk;
+    size_t n = 0;
+    if (with_state) n += sizeof(float) * (size_t)B * 3 * D * P + sizeof(float) * (size_t)B * P;
+    n += sizeof(uint32_t) * 6 * (size_t)B * P;           // rng SoA
+    n += (sizeof(uint32_t) + sizeof(int32_t)) * 2 * B * C;  // partial keys/idx
+    n += sizeof(float) * 2 * B * C * D;                   // partial vectors
+    n += (sizeof(uint32_t) + sizeof(int32_t)) * 2 * B;      // global best key/idx
+    n += sizeof(float) * 2 * B * D;                       // global best vector
+    return n + 8 * 256;                                   // alignment slack
+}
+
 
 }  // namespace ikpso

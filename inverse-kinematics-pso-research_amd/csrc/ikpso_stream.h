@@ -1,4 +1,4 @@
-// ikpso_stream.hip -- streaming variant of the swarm solve for swarms larger
+// ikpso_stream.h -- streaming variant of the swarm solve for swarms larger
 // than one workgroup (the visualiser's default N = 16384, src/Main.cpp:17) and
 // for long chains (BASELINE config 5: D = 60, P = 4096).
 //
@@ -11,6 +11,8 @@
 // slot t&1, and every workgroup of the NEXT launch reduces those partials and
 // applies the `globalMin > currentGlobalMin` update (src/kernel.cu:318)
 // redundantly -- the kernel boundary is the only cross-workgroup ordering.
+#pragma once
+
 #include <hip/hip_runtime.h>
 
 #include "ikpso_device.h"
@@ -256,7 +258,7 @@ __global__ void __launch_bounds__(kStreamChunk) k_stream_finalize(const ChainCon
 }
 
 template <class Topo, int MODE, int TERMS>
-static hipError_t run_stream(const ChainHost& ch, StreamIO io, int iterations, hipStream_t stream)
+inline hipError_t run_stream(const ChainHost& ch, StreamIO io, int iterations, hipStream_t stream)
 {
     const ChainConsts<Topo::J> cc = make_consts<Topo::J>(ch);
     const dim3 grid((unsigned)(io.num_swarms * io.C)), threads(kStreamChunk);
@@ -272,55 +274,18 @@ static hipError_t run_stream(const ChainHost& ch, StreamIO io, int iterations, h
 }
 
 template <class Topo, int MODE>
-static hipError_t run_stream_terms(const ChainHost& ch, const StreamIO& io, int iterations, hipStream_t stream)
+inline hipError_t run_stream_terms(const ChainHost& ch, const StreamIO& io, int iterations, hipStream_t stream)
 {
-    if constexpr (Topo::kGeneric) {
-        return run_stream<Topo, MODE, kTermRuntime>(ch, io, iterations, stream);
-    } else {
-        switch ((ch.use_posref ? kTermPosRef : 0) | (ch.use_penalty ? kTermPenalty : 0) |
-                (ch.uniform_bounds ? kTermUniformBounds : 0)) {
-        case kTermUniformBounds: return run_stream<Topo, MODE, kTermUniformBounds>(ch, io, iterations, stream);
-        case kTermUniformBounds | kTermPenalty:
+    // Same term specialisation as run_resident.
+    const int terms = (ch.use_posref ? kTermPosRef : 0) | (ch.use_penalty ? kTermPenalty : 0) |
+                      (ch.uniform_bounds ? kTermUniformBounds : 0);
+    if constexpr (!Topo::kGeneric && MODE == IKPSO_ARITH_FAST) {
+        if (terms == kTermUniformBounds) return run_stream<Topo, MODE, kTermUniformBounds>(ch, io, iterations, stream);
+        if (terms == (kTermUniformBounds | kTermPenalty))
             return run_stream<Topo, MODE, kTermUniformBounds | kTermPenalty>(ch, io, iterations, stream);
-        case kTermUniformBounds | kTermPosRef: return run_stream<Topo, MODE, 1>(ch, io, iterations, stream);
-        case kTermUniformBounds | kTermPosRef | kTermPenalty:
-            return run_stream<Topo, MODE, 3>(ch, io, iterations, stream);
-        case 0: return run_stream<Topo, MODE, 0>(ch, io, iterations, stream);
-        case 1: return run_stream<Topo, MODE, 1>(ch, io, iterations, stream);
-        case 2: return run_stream<Topo, MODE, 2>(ch, io, iterations, stream);
-        default: return run_stream<Topo, MODE, 3>(ch, io, iterations, stream);
-        }
     }
-}
-
-hipError_t launch_stream(const ChainHost& ch, int mode, const StreamIO& io, int iterations, hipStream_t stream)
-{
-    if (io.num_swarms <= 0) return hipSuccess;
-    if (!ch.aux_dev || io.C != (io.P + kStreamChunk - 1) / kStreamChunk) return hipErrorInvalidValue;
-    hipError_t err = hipErrorInvalidValue;
-    const bool ok = visit_topology(ch, [&](auto topo) {
-        using T = decltype(topo);
-        if (mode == IKPSO_ARITH_REFERENCE)
-            err = run_stream_terms<T, IKPSO_ARITH_REFERENCE>(ch, io, iterations, stream);
-        else
-            err = run_stream_terms<T, IKPSO_ARITH_FAST>(ch, io, iterations, stream);
-    });
-    return ok ? err : hipErrorInvalidValue;
-}
-
-// Workspace bytes for B swarms of P particles and D angles (state excluded when
-// the caller provides it).
-size_t stream_workspace_bytes(int64_t B, int P, int D, bool with_state)
-{
-    const int64_t C = (P + kStreamChunk - 1) / kStreamChunk;
-    size_t n = 0;
-    if (with_state) n += sizeof(float) * (size_t)B * 3 * D * P + sizeof(float) * (size_t)B * P;
-    n += sizeof(uint32_t) * 6 * (size_t)B * P;           // rng SoA
-    n += (sizeof(uint32_t) + sizeof(int32_t)) * 2 * B * C;  // partial keys/idx
-    n += sizeof(float) * 2 * B * C * D;                   // partial vectors
-    n += (sizeof(uint32_t) + sizeof(int32_t)) * 2 * B;      // global best key/idx
-    n += sizeof(float) * 2 * B * D;                       // global best vector
-    return n + 8 * 256;                                   // alignment slack
+    (void)terms;
+    return run_stream<Topo, MODE, kTermRuntime>(ch, io, iterations, stream);
 }
 
 }  // namespace ikpso

@@ -1,0 +1,39 @@
+// ikpso_topo_ops.h -- per-topology launch entry points.  The kernel templates
+// (ikpso_resident.h, ikpso_stream.h) are instantiated per (topology, mode) in
+// their own translation units (ikpso_inst_*.hip) so the build parallelises;
+// the dispatcher (ikpso_kernels.hip) sees only these declarations.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "ikpso_kernels.h"
+
+namespace ikpso {
+
+template <class Topo, int MODE>
+struct ModeOps {
+    static hipError_t resident(const ChainHost& ch, const SwarmIO& io, int block, hipStream_t stream);
+    static hipError_t stream(const ChainHost& ch, const StreamIO& io, int iterations, hipStream_t stream);
+    static hipError_t evaluate(const ChainHost& ch, const EvalIO& io, hipStream_t stream);
+};
+
+template <class Topo>
+struct TopoOps {
+    static hipError_t resident(const ChainHost& ch, int mode, const SwarmIO& io, int block, hipStream_t s)
+    {
+        return mode == IKPSO_ARITH_REFERENCE ? ModeOps<Topo, IKPSO_ARITH_REFERENCE>::resident(ch, io, block, s)
+                                             : ModeOps<Topo, IKPSO_ARITH_FAST>::resident(ch, io, block, s);
+    }
+    static hipError_t stream(const ChainHost& ch, int mode, const StreamIO& io, int iterations, hipStream_t s)
+    {
+        return mode == IKPSO_ARITH_REFERENCE ? ModeOps<Topo, IKPSO_ARITH_REFERENCE>::stream(ch, io, iterations, s)
+                                             : ModeOps<Topo, IKPSO_ARITH_FAST>::stream(ch, io, iterations, s);
+    }
+    static hipError_t evaluate(const ChainHost& ch, int mode, const EvalIO& io, hipStream_t s)
+    {
+        return mode == IKPSO_ARITH_REFERENCE ? ModeOps<Topo, IKPSO_ARITH_REFERENCE>::evaluate(ch, io, s)
+                                             : ModeOps<Topo, IKPSO_ARITH_FAST>::evaluate(ch, io, s);
+    }
+};
+
+}  // namespace ikpso
