@@ -25,13 +25,13 @@
 extern "C" {
 #endif
 
-#define IKPSO_ABI_VERSION 1
+#define IKPSO_ABI_VERSION 2
 
 typedef int ikpso_status;
 enum {
     IKPSO_OK = 0,
     IKPSO_ERR_INVALID_ARG = 1,   /* bad size, null pointer, bad node table */
-    IKPSO_ERR_UNSUPPORTED = 2,   /* e.g. colliderCount > 0 (GJK term not built yet) */
+    IKPSO_ERR_UNSUPPORTED = 2,   /* no compiled kernel for this chain / swarm size / kernel family */
     IKPSO_ERR_HIP = 3,           /* a HIP runtime call failed; see ikpso_last_hip_error() */
     IKPSO_ERR_NO_MEMORY = 4
 };
@@ -83,7 +83,8 @@ typedef struct ikpso_fitness_config {
     float error_threshold; /* never read, as in the reference */
 } ikpso_fitness_config;
 
-/* obj_t (src/BoxCollider.h:4-10): box half-extents, centre, orientation quaternion. */
+/* obj_t (src/BoxCollider.h:4-10): box edge lengths x, y, z (supportBox uses
+ * +-x/2), centre, orientation quaternion (x, y, z, w). */
 typedef struct ikpso_collider {
     float x, y, z;
     float pos[3];
@@ -125,7 +126,8 @@ ikpso_status ikpso_init_generators_seeded(ikpso_rng_state* randoms, int64_t coun
  *   randoms   [size] states, device: consumed and advanced (persist across calls).
  *   chain     [node_count] nodes, any.  D = 3*(node_count-1).
  *   result    [D] floats, any: global-best joint angles (Coordinates).
- *   colliders/collider_count: collider_count must be 0 (IKPSO_ERR_UNSUPPORTED otherwise).
+ *   colliders [collider_count] obj_t, any: boxes of the collider term (src/kernel.cu:104-136):
+ *             a particle whose node or link box intersects one (GJK) gets fitness FLT_MAX.
  * Synchronises `stream` before returning. */
 ikpso_status ikpso_calculate_pso(float* particles, const float* positions, float* bests,
                                  ikpso_rng_state* randoms, int size, const ikpso_node* chain, int node_count,
@@ -153,6 +155,10 @@ typedef struct ikpso_solver_desc {
     float reserved1;
     const float* soft_lo;     /* any, [D] or NULL */
     const float* soft_hi;     /* any, [D] or NULL */
+    /* Collider term, as calculatePSO's colliders/colliderCount (ABI >= 2). */
+    const ikpso_collider* colliders; /* any, [collider_count] or NULL */
+    int32_t collider_count;
+    int32_t reserved2;
 } ikpso_solver_desc;
 
 ikpso_status ikpso_solver_create(const ikpso_solver_desc* desc, ikpso_solver** out);

@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 
 #include <math.h>
+
+#include <cmath>
 #include <stdlib.h>
 #include <string.h>
 
@@ -120,7 +122,35 @@ struct Extras {
     float limit_weight = 0.0f;
     const float* soft_lo = nullptr;    // host copies, [D]
     const float* soft_hi = nullptr;
+    const ikpso_collider* colliders = nullptr;  // host copy, [collider_count]
+    int collider_count = 0;
 };
+
+// Device record of one obj_t collider (ikpso_collide.h): the inverse
+// quaternion is quatInvert2's (same fp32 operations as the device would do)
+// and the radius bounds every support point of the box.
+CollRec collider_record(const ikpso_collider& c)
+{
+    CollRec r{};
+    r.px = c.pos[0];
+    r.py = c.pos[1];
+    r.pz = c.pos[2];
+    r.qx = c.quat[0];
+    r.qy = c.quat[1];
+    r.qz = c.quat[2];
+    r.qw = c.quat[3];
+    float qi[4];
+    quat_inverse(c.quat, qi);
+    r.ix = qi[0];
+    r.iy = qi[1];
+    r.iz = qi[2];
+    r.iw = qi[3];
+    r.sx = c.x;
+    r.sy = c.y;
+    r.sz = c.z;
+    r.radius = sphere_radius(fabsf(c.x), fabsf(c.y), fabsf(c.z), quat_gain(c.quat[0], c.quat[1], c.quat[2], c.quat[3]));
+    return r;
+}
 
 ikpso_status parse_chain(const std::vector<ikpso_node>& nodes, const ikpso_pso_config& pso,
                          const ikpso_fitness_config& fit, const Extras& ex, ChainHost& ch)
@@ -185,7 +215,16 @@ ikpso_status parse_chain(const std::vector<ikpso_node>& nodes, const ikpso_pso_c
     ch.use_posref = fit.distance_weight != 0.0f;
     ch.lim_w = ex.limit_weight;
     ch.use_penalty = ex.limit_weight != 0.0f && ex.soft_lo && ex.soft_hi;
-    ch.aux.assign(10 * J, 0.0f);
+    // aux = [posref 4J | soft_lo 3J | soft_hi 3J | pad to 16 floats | collider records]
+    ch.num_coll = ex.collider_count;
+    ch.coll_off = ((size_t)10 * J + 15) & ~size_t(15);
+    ch.aux.assign(ch.coll_off + (size_t)16 * ch.num_coll, 0.0f);
+    for (int i = 0; i < ch.num_coll; ++i) {
+        const CollRec r = collider_record(ex.colliders[i]);
+        memcpy(ch.aux.data() + ch.coll_off + 16 * (size_t)i, &r, sizeof(r));
+        if (!std::isfinite(r.radius) || !std::isfinite(r.px) || !std::isfinite(r.py) || !std::isfinite(r.pz))
+            return IKPSO_ERR_INVALID_ARG;
+    }
     if (ch.use_posref && ex.positions)
         for (int i = 0; i < 4 * J; ++i) ch.aux[i] = ex.positions[i];
     if (ch.use_penalty)
@@ -323,8 +362,7 @@ ikpso_status ikpso_calculate_pso(float* particles, const float* positions, float
                                  ikpso_fitness_config fit, float* result, const ikpso_collider* colliders,
                                  int collider_count, void* stream)
 {
-    (void)colliders;
-    if (collider_count > 0) return IKPSO_ERR_UNSUPPORTED;  // GJK term: not built yet
+    if (collider_count < 0 || (collider_count > 0 && !colliders)) return IKPSO_ERR_INVALID_ARG;
     if (size <= 0 || !particles || !bests || !randoms || !chain || !result || node_count < 2 ||
         node_count - 1 > kMaxJoints || pso.iterations < 0)
         return IKPSO_ERR_INVALID_ARG;
@@ -340,6 +378,13 @@ ikpso_status ikpso_calculate_pso(float* particles, const float* positions, float
         if (st != IKPSO_OK) return st;
         ex.positions = pos.data();
     }
+    std::vector<ikpso_collider> boxes(collider_count);
+    if (collider_count > 0) {
+        st = fetch_any(boxes.data(), colliders, sizeof(ikpso_collider) * collider_count);
+        if (st != IKPSO_OK) return st;
+        ex.colliders = boxes.data();
+        ex.collider_count = collider_count;
+    }
     ChainHost ch;
     st = parse_chain(nodes, pso, fit, ex, ch);
     if (st != IKPSO_OK) return st;
@@ -351,17 +396,18 @@ ikpso_status ikpso_calculate_pso(float* particles, const float* positions, float
     const int mode = (env && strcmp(env, "reference") == 0) ? IKPSO_ARITH_REFERENCE : IKPSO_ARITH_FAST;
 
     std::lock_guard<std::mutex> lk(g_scratch_mu);
-    // device scratch: [result D | aux 10J | streaming workspace]; aux is
-    // uploaded here and the call synchronises before returning, so `ch.aux`
-    // outlives every use
-    const size_t head = sizeof(float) * (D + ch.aux.size());
+    // device scratch: [result D | aux (64-float aligned) | streaming workspace];
+    // aux is uploaded here and the call synchronises before returning, so
+    // `ch.aux` outlives every use
+    const size_t aux_at = ((size_t)D + 63) & ~size_t(63);
+    const size_t head = sizeof(float) * (aux_at + ch.aux.size());
     const size_t ws = family == IKPSO_KERNEL_STREAMING ? stream_workspace_bytes(1, size, D, false) : 0;
     float* dres = nullptr;
     st = scratch(((head + 255) & ~size_t(255)) + ws, &dres);
     if (st != IKPSO_OK) return st;
     const hipStream_t s = (hipStream_t)stream;
-    IKPSO_HIP(hipMemcpyAsync(dres + D, ch.aux.data(), sizeof(float) * ch.aux.size(), hipMemcpyHostToDevice, s));
-    ch.aux_dev = dres + D;
+    IKPSO_HIP(hipMemcpyAsync(dres + aux_at, ch.aux.data(), sizeof(float) * ch.aux.size(), hipMemcpyHostToDevice, s));
+    ch.aux_dev = dres + aux_at;
     if (family == IKPSO_KERNEL_RESIDENT) {
         SwarmIO io{};
         io.rng = randoms;
@@ -413,6 +459,15 @@ ikpso_status ikpso_solver_create(const ikpso_solver_desc* desc, ikpso_solver** o
         ex.limit_weight = desc->limit_weight;
         ex.soft_lo = slo.data();
         ex.soft_hi = shi.data();
+    }
+    std::vector<ikpso_collider> boxes;
+    if (desc->collider_count < 0 || (desc->collider_count > 0 && !desc->colliders)) return IKPSO_ERR_INVALID_ARG;
+    if (desc->collider_count > 0) {
+        boxes.resize(desc->collider_count);
+        if ((st = fetch_any(boxes.data(), desc->colliders, sizeof(ikpso_collider) * boxes.size())) != IKPSO_OK)
+            return st;
+        ex.colliders = boxes.data();
+        ex.collider_count = desc->collider_count;
     }
     ikpso_solver* s = new (std::nothrow) ikpso_solver();
     if (!s) return IKPSO_ERR_NO_MEMORY;

@@ -5,7 +5,7 @@
 //   XORWOW generator            curand_init/curand_uniform used at src/utility_kernels.cuh:28,
 //                               src/kernel.cu:164-166,261
 //   forward kinematics          updateChainMatrices src/kernel.cu:31-62 + src/matrix_operations.cuh
-//   fitness                     calculateDistance src/kernel.cu:64-151 (collider branch excluded)
+//   fitness                     calculateDistance src/kernel.cu:64-151 (collider block: ikpso_collide.h)
 //   velocity/position update    simulateParticlesKernel src/kernel.cu:153-189
 //   swarm argmin                thrust::min_element src/kernel.cu:297,315 (first minimum)
 #pragma once
@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "ikpso_collide.h"
 #include "ikpso_params.h"
 
 #ifndef IKPSO_SCHED_NODE
@@ -329,17 +330,19 @@ __device__ __forceinline__ Frame child_frame(const Frame& P, float a, float b, f
 // kTermUniformBounds: every angle has the same clamp bounds (the reference
 // scene: [0, 2pi] on every axis), read once from the kernarg into SGPRs
 // instead of per dimension from LDS.
-constexpr int kTermPosRef = 1, kTermPenalty = 2, kTermRuntime = 4, kTermUniformBounds = 8;
+// kTermColliders: the collider (GJK) block of calculateDistance
+// (src/kernel.cu:104-136), compiled in only when the scene has colliders.
+constexpr int kTermPosRef = 1, kTermPenalty = 2, kTermRuntime = 4, kTermUniformBounds = 8, kTermColliders = 16;
 
 template <class Topo, int MODE, int TERMS>
 struct FitnessAcc {
     static constexpr int J = Topo::J;
     Frame F[J + 1];
     float rot_diff, pos_diff, distance, pen;
-    bool posref, penalty;
+    bool hit, posref, penalty;
 
     __device__ __forceinline__ explicit FitnessAcc(const ChainConsts<J>& cc)
-        : rot_diff(0.0f), pos_diff(0.0f), distance(0.0f), pen(0.0f),
+        : rot_diff(0.0f), pos_diff(0.0f), distance(0.0f), pen(0.0f), hit(false),
           posref((TERMS & kTermPosRef) || ((TERMS & kTermRuntime) && cc.use_posref)),
           penalty((TERMS & kTermPenalty) || ((TERMS & kTermRuntime) && cc.use_penalty))
     {
@@ -390,6 +393,14 @@ struct FitnessAcc {
                 pen = pen + over * over;
             }
         }
+        if constexpr (TERMS & kTermColliders) {
+            // any node/link box hit -> FLT_MAX (the reference returns at the
+            // first hit; later nodes cannot change that)
+            if (!hit)
+                hit = node_collides(F[k].r00, F[k].r01, F[k].r02, F[k].r10, F[k].r11, F[k].r12, F[k].r20, F[k].r21,
+                                    F[k].r22, F[k].px, F[k].py, F[k].pz, F[pk].px, F[pk].py, F[pk].pz, cc.len[k],
+                                    cc.coll, cc.num_coll);
+        }
         if (node_pos) {
             node_pos[3 * (k - 1) + 0] = F[k].px;
             node_pos[3 * (k - 1) + 1] = F[k].py;
@@ -402,6 +413,7 @@ struct FitnessAcc {
 #pragma clang fp contract(off)
         float f = posref ? (distance + cc.dw_j * pos_diff) + cc.aw_j * rot_diff : distance + cc.aw_j * rot_diff;
         if (penalty) f = f + cc.lim_w * pen;
+        if constexpr (TERMS & kTermColliders) f = hit ? FLT_MAX : f;
         return f;
     }
 };

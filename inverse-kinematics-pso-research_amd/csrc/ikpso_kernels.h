@@ -9,6 +9,7 @@
 #include <vector>
 
 #include "ikpso.h"
+#include "ikpso_collide.h"
 #include "ikpso_params.h"
 
 namespace ikpso {
@@ -24,12 +25,15 @@ struct ChainHost {
     TopoKind topo = TopoKind::Generic;
     std::vector<int> parent, eff_slot;
     std::vector<float> len, eff_w, lo, hi, rest, tgt0;
-    std::vector<float> aux;          // [posref 4J | soft_lo 3J | soft_hi 3J] (host copy)
+    // [posref 4J | soft_lo 3J | soft_hi 3J | collider records 16*num_coll] (host copy)
+    std::vector<float> aux;
     const float* aux_dev = nullptr;  // device copy, owned by the solver / call
     float m0[12] = {};
     float w = 0, c1 = 0, c2 = 0, aw_j = 0, dw_j = 0, lim_w = 0;
     bool use_posref = false, use_penalty = false;
     bool uniform_bounds = false;  // every angle has clamp bounds lo[0], hi[0]
+    int num_coll = 0;             // colliders (obj_t) of the scene
+    size_t coll_off = 0;          // float offset of the collider records in aux
 };
 
 // Evaluate-kernel parameters.
@@ -85,6 +89,8 @@ ChainConsts<J> make_consts(const ChainHost& h)
     c.use_posref = h.use_posref ? 1 : 0;
     c.use_penalty = h.use_penalty ? 1 : 0;
     c.num_eff = h.E;
+    c.num_coll = h.num_coll;
+    c.coll = h.num_coll && h.aux_dev ? reinterpret_cast<const CollRec*>(h.aux_dev + h.coll_off) : nullptr;
     return c;
 }
 

@@ -33,6 +33,8 @@ struct ChainConsts {
     float aw_j, dw_j, lim_w;  // angleWeight/J, distanceWeight/J, limit weight
     int32_t use_posref, use_penalty;
     int32_t num_eff;
+    int32_t num_coll;         // colliders (kTermColliders kernels only)
+    const struct CollRec* coll;  // [num_coll] device records, inside the aux buffer
 };
 
 // Per-launch buffers.

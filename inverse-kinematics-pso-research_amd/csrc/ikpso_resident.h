@@ -164,7 +164,7 @@ __global__ void __launch_bounds__(kResidentMaxThreads<Topo::J>())
 }
 
 // ----------------------------------------------------------- evaluate kernel
-template <class Topo, int MODE>
+template <class Topo, int MODE, int TERMS>
 __global__ void __launch_bounds__(256) k_evaluate(const ChainConsts<Topo::J> cc, EvalIO io)
 {
     constexpr int J = Topo::J;
@@ -189,7 +189,7 @@ __global__ void __launch_bounds__(256) k_evaluate(const ChainConsts<Topo::J> cc,
 #pragma unroll
             for (int d = 0; d < D; ++d) tgt[d] = cc.tgt0[d];
         }
-        const float f = fitness<Topo, MODE, kTermRuntime>(cc, x, rest, tgt, pos);
+        const float f = fitness<Topo, MODE, TERMS>(cc, x, rest, tgt, pos);
         if (io.out_fitness) io.out_fitness[n] = f;
         if (io.out_positions) {
 #pragma unroll
@@ -208,9 +208,10 @@ inline hipError_t run_resident(const ChainHost& ch, const SwarmIO& io, int block
     // reference scene (uniform clamp bounds, no optional term) and BASELINE
     // config 5 (uniform bounds + soft-limit penalty) -- get their own FAST
     // kernels; everything else (generic topologies, the distance term, every
-    // REFERENCE-mode run) tests the terms at run time with the same arithmetic.
+    // REFERENCE-mode run) tests the terms at run time with the same arithmetic,
+    // with the collider block compiled in only when the scene has colliders.
     const int terms = (ch.use_posref ? kTermPosRef : 0) | (ch.use_penalty ? kTermPenalty : 0) |
-                      (ch.uniform_bounds ? kTermUniformBounds : 0);
+                      (ch.uniform_bounds ? kTermUniformBounds : 0) | (ch.num_coll > 0 ? kTermColliders : 0);
     if constexpr (!Topo::kGeneric && MODE == IKPSO_ARITH_FAST) {
         if (terms == kTermUniformBounds) {
             hipLaunchKernelGGL((k_swarm_resident<Topo, MODE, kTermUniformBounds>), grid, threads, 0, stream, cc, io);
@@ -223,7 +224,11 @@ inline hipError_t run_resident(const ChainHost& ch, const SwarmIO& io, int block
         }
     }
     (void)terms;
-    hipLaunchKernelGGL((k_swarm_resident<Topo, MODE, kTermRuntime>), grid, threads, 0, stream, cc, io);
+    if (ch.num_coll > 0)
+        hipLaunchKernelGGL((k_swarm_resident<Topo, MODE, kTermRuntime | kTermColliders>), grid, threads, 0, stream, cc,
+                           io);
+    else
+        hipLaunchKernelGGL((k_swarm_resident<Topo, MODE, kTermRuntime>), grid, threads, 0, stream, cc, io);
     return hipGetLastError();
 }
 
@@ -234,7 +239,12 @@ inline hipError_t run_evaluate(const ChainHost& ch, const EvalIO& io, hipStream_
     int64_t blocks = (io.n + 255) / 256;
     if (blocks > 8192) blocks = 8192;
     if (blocks < 1) blocks = 1;
-    hipLaunchKernelGGL((k_evaluate<Topo, MODE>), dim3((unsigned)blocks), dim3(256), 0, stream, cc, io);
+    if (ch.num_coll > 0)
+        hipLaunchKernelGGL((k_evaluate<Topo, MODE, kTermRuntime | kTermColliders>), dim3((unsigned)blocks), dim3(256),
+                           0, stream, cc, io);
+    else
+        hipLaunchKernelGGL((k_evaluate<Topo, MODE, kTermRuntime>), dim3((unsigned)blocks), dim3(256), 0, stream, cc,
+                           io);
     return hipGetLastError();
 }
 

@@ -278,13 +278,14 @@ inline hipError_t run_stream_terms(const ChainHost& ch, const StreamIO& io, int 
 {
     // Same term specialisation as run_resident.
     const int terms = (ch.use_posref ? kTermPosRef : 0) | (ch.use_penalty ? kTermPenalty : 0) |
-                      (ch.uniform_bounds ? kTermUniformBounds : 0);
+                      (ch.uniform_bounds ? kTermUniformBounds : 0) | (ch.num_coll > 0 ? kTermColliders : 0);
     if constexpr (!Topo::kGeneric && MODE == IKPSO_ARITH_FAST) {
         if (terms == kTermUniformBounds) return run_stream<Topo, MODE, kTermUniformBounds>(ch, io, iterations, stream);
         if (terms == (kTermUniformBounds | kTermPenalty))
             return run_stream<Topo, MODE, kTermUniformBounds | kTermPenalty>(ch, io, iterations, stream);
     }
     (void)terms;
+    if (ch.num_coll > 0) return run_stream<Topo, MODE, kTermRuntime | kTermColliders>(ch, io, iterations, stream);
     return run_stream<Topo, MODE, kTermRuntime>(ch, io, iterations, stream);
 }
 

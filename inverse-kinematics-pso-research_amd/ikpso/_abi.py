@@ -65,6 +65,14 @@ RNG_DTYPE = np.dtype(
 assert RNG_DTYPE.itemsize == 48
 RNG_WORDS = 12  # int32 words per state
 
+#: obj_t (src/BoxCollider.h:4-10), 48 bytes: edge lengths x, y, z; centre; quaternion (x, y, z, w).
+COLLIDER_DTYPE = np.dtype(
+    [("x", "<f4"), ("y", "<f4"), ("z", "<f4"), ("pos", "<f4", (3,)), ("pad_", "<f4", (2,)), ("quat", "<f4", (4,))]
+)
+assert COLLIDER_DTYPE.itemsize == 48
+
+ABI_VERSION = 2
+
 
 # ------------------------------------------------------------ ctypes structs
 class PSOConfig(ctypes.Structure):
@@ -102,6 +110,9 @@ class SolverDesc(ctypes.Structure):
         ("reserved1", ctypes.c_float),
         ("soft_lo", ctypes.c_void_p),
         ("soft_hi", ctypes.c_void_p),
+        ("colliders", ctypes.c_void_p),
+        ("collider_count", ctypes.c_int32),
+        ("reserved2", ctypes.c_int32),
     ]
 
 
@@ -158,6 +169,8 @@ def load() -> ctypes.CDLL:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    if lib.ikpso_abi_version() != ABI_VERSION:
+        raise RuntimeError(f"{path}: ABI version {lib.ikpso_abi_version()}, expected {ABI_VERSION} (rebuild)")
     _LIB = lib
     return lib
 

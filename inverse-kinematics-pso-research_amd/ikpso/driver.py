@@ -65,7 +65,7 @@ class FrameDriver:
     the arm, count frames until the effector distance sum <= eps)."""
 
     def __init__(self, particles: int = 16384, pso: PSOConfig = MAIN_PSO, fit: FitnessConfig = MAIN_FITNESS,
-                 scene: Optional[Scene] = None, log_dir: Optional[str] = None, device="cuda"):
+                 scene: Optional[Scene] = None, log_dir: Optional[str] = None, device="cuda", colliders=None):
         import torch
 
         self.torch = torch
@@ -82,12 +82,15 @@ class FrameDriver:
         if st != 0:
             raise RuntimeError(f"initGenerators failed ({st})")
         self.log = DiagnosticsLog(log_dir) if log_dir else None
+        # obj_t colliders (initColliders, src/Main.cpp:140-144); none by default, as src/Main.cpp:18
+        self.colliders = colliders
 
     def solve_frame(self) -> None:
         chain = self.scene.origin.to_cuda()
         positions = self.scene.origin.fill_positions()
+        nc = 0 if self.colliders is None else len(self.colliders)
         st = calculate_pso(self.particles, positions, self.bests, self.randoms, self.N, chain, self.pso, self.fit,
-                           self.result)
+                           self.result, self.colliders if nc else None, nc)
         if st != 0:  # the frame loop breaks on a failed solve (src/Main.cpp:226)
             raise RuntimeError(f"calculatePSO failed ({st})")
         self.scene.origin.from_coords(self.result)

@@ -245,3 +245,20 @@ def serial_chain(joints: int, length: float, rotation=(0.0, 0.3, 0.0), lo: float
             n = Node(rotation, (lo,) * 3, (hi,) * 3, length)
         parent = parent.attach_child(n)
     return origin
+
+
+def init_colliders(count: int) -> np.ndarray:
+    """initColliders (src/Main.cpp:537-559): the visualiser's first `count`
+    (<= 4) unit-cube colliders, as an obj_t (COLLIDER_DTYPE) array.  The
+    reference ships with colliderCount = 0 (src/Main.cpp:18)."""
+    from ._abi import COLLIDER_DTYPE
+
+    spec = [((1.0, 0.0, 0.0), (0.0, 0.0, 0.0, 1.0)),
+            ((0.0, 0.0, -1.0), (-0.403, -0.819, 0.273, 0.304)),
+            ((-1.0, 0.0, 0.0), (0.0, 0.0, 0.0, 1.0)),
+            ((0.0, 0.0, 1.0), (0.0, 0.0, 0.0, 1.0))]
+    out = np.zeros(max(0, min(int(count), 4)), dtype=COLLIDER_DTYPE)
+    for i in range(out.shape[0]):
+        out[i]["x"] = out[i]["y"] = out[i]["z"] = 1.0
+        out[i]["pos"], out[i]["quat"] = spec[i]
+    return out

@@ -95,6 +95,25 @@ def _stream_handle(stream) -> Optional[int]:
     return stream.cuda_stream or None
 
 
+def _colliders(colliders) -> np.ndarray:
+    """obj_t array (COLLIDER_DTYPE) from a compatible numpy array."""
+    b = np.ascontiguousarray(colliders)
+    if b.dtype != _abi.COLLIDER_DTYPE:
+        if b.dtype.itemsize != _abi.COLLIDER_DTYPE.itemsize:
+            raise TypeError("colliders must be an obj_t (COLLIDER_DTYPE) array")
+        b = b.view(_abi.COLLIDER_DTYPE)
+    return b.reshape(-1)
+
+
+def make_collider(size, pos, quat=(0.0, 0.0, 0.0, 1.0)) -> np.ndarray:
+    """One obj_t: size = (x, y, z) box edge lengths, pos = centre, quat = (x, y, z, w)."""
+    c = np.zeros(1, dtype=_abi.COLLIDER_DTYPE)
+    c["x"], c["y"], c["z"] = size
+    c["pos"] = pos
+    c["quat"] = quat
+    return c
+
+
 def rng_tensor(count: int, device="cuda"):
     """Device buffer for `count` generator states (48 bytes each, curandState_t layout)."""
     torch = _torch()
@@ -122,9 +141,13 @@ def calculate_pso(particles, positions, bests, randoms, size: int, chain: np.nda
                   fit_config: FitnessConfig, result, colliders=None, collider_count: int = 0, stream=None) -> int:
     """calculatePSO over the C ABI; same arguments, same meaning, same status
     convention.  `chain` is a NODE_DTYPE array (host) or device tensor;
-    `result` receives the global-best angles (numpy array or tensor)."""
+    `result` receives the global-best angles (numpy array or tensor);
+    `colliders` an obj_t array (numpy COLLIDER_DTYPE or a device tensor) with
+    `collider_count` entries (src/kernel.cu:104-136)."""
     lib = _abi.load()
     keep: list = []
+    if isinstance(colliders, np.ndarray):
+        colliders = _colliders(colliders)
     if isinstance(chain, np.ndarray):
         if chain.dtype != NODE_DTYPE:
             raise TypeError("chain must be an ikpso NODE_DTYPE array")
@@ -147,7 +170,7 @@ class BatchSolver:
 
     def __init__(self, chain: np.ndarray, particles: int, pso: PSOConfig = MAIN_PSO,
                  fit: FitnessConfig = MAIN_FITNESS, arith: str = "fast", positions=None,
-                 limit_weight: float = 0.0, soft_lo=None, soft_hi=None, kernel: str = "auto"):
+                 limit_weight: float = 0.0, soft_lo=None, soft_hi=None, kernel: str = "auto", colliders=None):
         self._lib = _abi.load()
         if chain.dtype != NODE_DTYPE:
             raise TypeError("chain must be an ikpso NODE_DTYPE array")
@@ -169,6 +192,10 @@ class BatchSolver:
         desc.limit_weight = float(limit_weight)
         desc.soft_lo = _any_ptr(None if soft_lo is None else np.asarray(soft_lo, np.float32), keep)
         desc.soft_hi = _any_ptr(None if soft_hi is None else np.asarray(soft_hi, np.float32), keep)
+        if colliders is not None and len(colliders):
+            boxes = _colliders(colliders)
+            desc.colliders = _any_ptr(boxes, keep)
+            desc.collider_count = int(boxes.shape[0])
         handle = ctypes.c_void_p()
         _abi.check(self._lib.ikpso_solver_create(ctypes.byref(desc), ctypes.byref(handle)), "ikpso_solver_create")
         self._h = handle

@@ -23,6 +23,7 @@
  *   - randInitKernel/initGenerators src/utility_kernels.cuh:21-47 -> orc_init_generators()
  *   - EffectorNode::calculateDistance / checkDistance src/Node.h:421-429,
  *     src/Main.cpp:290-298       -> orc_residual()
+ *   - the collider (GJK) block of calculateDistance src/kernel.cu:104-136 -> ikpso_gjk.c
  *
  * Third-party arithmetic restated from its published algorithm (not vendored
  * in the reference): cuRAND XORWOW (curand_init(seed,0,0), curand(),
@@ -248,9 +249,15 @@ typedef struct {
     float limit_weight;
     const float* soft_lo;
     const float* soft_hi;
-} orc_penalty;
+    /* collider term (src/kernel.cu:104-136; ikpso_gjk.c): obj_t[collider_count] */
+    const void* colliders;
+    int collider_count;
+} orc_extra;
 
-static float penalty_term(const orc_penalty* pen, const float* angles, int dof)
+/* ikpso_gjk.c */
+int orc_node_collides(const float* node, const float* parent, float length, const void* colliders, int count);
+
+static float penalty_term(const orc_extra* pen, const float* angles, int dof)
 {
     float p = 0.0f;
     for (int d = 0; d < dof; d++) {
@@ -261,9 +268,9 @@ static float penalty_term(const orc_penalty* pen, const float* angles, int dof)
 }
 
 static float fitness_pen(const orc_node* chain, int node_count, const float* positions, const float* angles,
-                         float angle_weight, float distance_weight, const orc_penalty* pen);
+                         float angle_weight, float distance_weight, const orc_extra* pen);
 
-/* calculateDistance (src/kernel.cu:64-151) with colliderCount = 0.
+/* calculateDistance (src/kernel.cu:64-151) with colliderCount = 0 (orc_fitness_ex: any).
  * angles contiguous [D]; positions = host-filled arm positions (read at slot (ind-1)*4). */
 float orc_fitness(const orc_node* chain, int node_count, const float* positions, const float* angles,
                   float angle_weight, float distance_weight)
@@ -273,15 +280,14 @@ float orc_fitness(const orc_node* chain, int node_count, const float* positions,
 
 float orc_fitness_ex(const orc_node* chain, int node_count, const float* positions, const float* angles,
                      float angle_weight, float distance_weight, float limit_weight, const float* soft_lo,
-                     const float* soft_hi)
+                     const float* soft_hi, const void* colliders, int collider_count)
 {
-    orc_penalty pen = {limit_weight, soft_lo, soft_hi};
-    return fitness_pen(chain, node_count, positions, angles, angle_weight, distance_weight,
-                       (limit_weight != 0.0f && soft_lo && soft_hi) ? &pen : NULL);
+    orc_extra pen = {limit_weight, soft_lo, soft_hi, colliders, collider_count};
+    return fitness_pen(chain, node_count, positions, angles, angle_weight, distance_weight, &pen);
 }
 
 static float fitness_pen(const orc_node* chain, int node_count, const float* positions, const float* angles,
-                         float angle_weight, float distance_weight, const orc_penalty* pen)
+                         float angle_weight, float distance_weight, const orc_extra* pen)
 {
     const int dof = 3 * (node_count - 1);
     float rot_diff = 0.0f, pos_diff = 0.0f, distance = 0.0f;
@@ -293,6 +299,13 @@ static float fitness_pen(const orc_node* chain, int node_count, const float* pos
         rot_diff = rot_diff + msq3(chain[ind].rotation[0] - a[0], chain[ind].rotation[1] - a[1],
                                    chain[ind].rotation[2] - a[2]);
         const float* M = mp + 16 * ind;
+        /* collider block (src/kernel.cu:104-136): any hit -> FLT_MAX */
+        if (pen && pen->collider_count > 0 &&
+            orc_node_collides(M, mp + 16 * chain[ind].parent_index, chain[ind].length, pen->colliders,
+                              pen->collider_count)) {
+            if (mp != mats) free(mp);
+            return FLT_MAX;
+        }
         /* multiplyMatByVec(model, (0,0,0,1)) */
         float px = M[0] * 0.0f + M[1] * 0.0f + M[2] * 0.0f + M[3] * 1.0f;
         float py = M[4] * 0.0f + M[5] * 0.0f + M[6] * 0.0f + M[7] * 1.0f;
@@ -312,12 +325,12 @@ static float fitness_pen(const orc_node* chain, int node_count, const float* pos
     if (mp != mats) free(mp);
     const float jn = (float)(dof / 3);
     float f = distance + distance_weight / jn * pos_diff + angle_weight / jn * rot_diff;
-    if (pen) f = f + penalty_term(pen, angles, dof);
+    if (pen && pen->limit_weight != 0.0f && pen->soft_lo && pen->soft_hi) f = f + penalty_term(pen, angles, dof);
     return f;
 }
 
 static float fitness_soa(const orc_node* chain, int node_count, const float* positions, const float* particles,
-                         int64_t count, int64_t i, float aw, float dw, const orc_penalty* pen)
+                         int64_t count, int64_t i, float aw, float dw, const orc_extra* pen)
 {
     const int dof = 3 * (node_count - 1);
     float ang[3 * 64];
@@ -364,13 +377,13 @@ static int64_t argmin_first(const float* v, int64_t n)
     return best;
 }
 
-/* calculatePSO (src/kernel.cu:279-327), colliderCount = 0.
+/* calculatePSO (src/kernel.cu:279-327); orc_calculate_pso: colliderCount = 0, _ex: any.
  * particles: [3][dof][size] SoA (position, velocity, localBest); bests[size];
  * randoms[size]; result[dof].  Returns 0. */
 static int calculate_pso_pen(float* particles, const float* positions, float* bests, orc_rng* randoms,
                              int64_t size, const orc_node* chain, int node_count, float inertia, float local,
                              float global, int iterations, float angle_weight, float distance_weight,
-                             float* result, const orc_penalty* pen);
+                             float* result, const orc_extra* pen);
 
 int orc_calculate_pso(float* particles, const float* positions, float* bests, orc_rng* randoms, int64_t size,
                       const orc_node* chain, int node_count, float inertia, float local, float global,
@@ -383,18 +396,18 @@ int orc_calculate_pso(float* particles, const float* positions, float* bests, or
 int orc_calculate_pso_ex(float* particles, const float* positions, float* bests, orc_rng* randoms, int64_t size,
                          const orc_node* chain, int node_count, float inertia, float local, float global,
                          int iterations, float angle_weight, float distance_weight, float* result,
-                         float limit_weight, const float* soft_lo, const float* soft_hi)
+                         float limit_weight, const float* soft_lo, const float* soft_hi, const void* colliders,
+                         int collider_count)
 {
-    orc_penalty pen = {limit_weight, soft_lo, soft_hi};
+    orc_extra pen = {limit_weight, soft_lo, soft_hi, colliders, collider_count};
     return calculate_pso_pen(particles, positions, bests, randoms, size, chain, node_count, inertia, local, global,
-                             iterations, angle_weight, distance_weight, result,
-                             (limit_weight != 0.0f && soft_lo && soft_hi) ? &pen : NULL);
+                             iterations, angle_weight, distance_weight, result, &pen);
 }
 
 static int calculate_pso_pen(float* particles, const float* positions, float* bests, orc_rng* randoms,
                              int64_t size, const orc_node* chain, int node_count, float inertia, float local,
                              float global, int iterations, float angle_weight, float distance_weight,
-                             float* result, const orc_penalty* pen)
+                             float* result, const orc_extra* pen)
 {
     const int dof = 3 * (node_count - 1);
     const int64_t n = size;
@@ -466,17 +479,19 @@ static int calculate_pso_pen(float* particles, const float* positions, float* be
  * rng: [B][P] states, persisting across calls.
  * Outputs: angles[B][D], fitness[B], residual[B] (residual may be NULL).
  * limit_weight/soft_lo/soft_hi: optional penalty extension (0/NULL = off).
+ * colliders/collider_count: obj_t boxes of the collider term (0 = off).
  * Parallel over swarms with OpenMP (threads <= 0: runtime default). */
 int orc_solve_batch(const orc_node* chain, int node_count, const float* targets, const float* start_pose,
                     int64_t num_swarms, int particles_per_swarm, int iterations, float inertia, float local,
                     float global, float angle_weight, float distance_weight, const float* positions,
                     orc_rng* rng, float* out_angles, float* out_fitness, float* out_residual, int threads,
-                    float limit_weight, const float* soft_lo, const float* soft_hi)
+                    float limit_weight, const float* soft_lo, const float* soft_hi, const void* colliders,
+                    int collider_count)
 {
     const int dof = 3 * (node_count - 1);
     const int64_t P = particles_per_swarm;
-    orc_penalty pen = {limit_weight, soft_lo, soft_hi};
-    const orc_penalty* penp = (limit_weight != 0.0f && soft_lo && soft_hi) ? &pen : NULL;
+    orc_extra pen = {limit_weight, soft_lo, soft_hi, colliders, collider_count};
+    const orc_extra* penp = &pen;
     int num_eff = 0;
     for (int k = 1; k < node_count; k++) num_eff += chain[k].node_type == ORC_EFFECTOR;
     if (node_count > 64 || node_count < 2) return 1;

@@ -32,6 +32,11 @@ RNG_DTYPE = np.dtype(
     ]
 )
 
+# obj_t (src/BoxCollider.h:4-10): x, y, z are the box's full edge lengths.
+BOX_DTYPE = np.dtype(
+    [("x", "<f4"), ("y", "<f4"), ("z", "<f4"), ("pos", "<f4", (3,)), ("pad_", "<f4", (2,)), ("quat", "<f4", (4,))]
+)
+
 _LIB = None
 _P = ctypes.c_void_p
 
@@ -58,7 +63,10 @@ def load():
             "orc_chain_matrices": (None, [_P, ctypes.c_int, _P, _P]),
             "orc_fitness": (ctypes.c_float, [_P, ctypes.c_int, _P, _P, ctypes.c_float, ctypes.c_float]),
             "orc_fitness_ex": (ctypes.c_float, [_P, ctypes.c_int, _P, _P, ctypes.c_float, ctypes.c_float,
-                                                ctypes.c_float, _P, _P]),
+                                                ctypes.c_float, _P, _P, _P, ctypes.c_int]),
+            "orc_sizeof_box": (ctypes.c_int, []),
+            "orc_gjk_intersect": (ctypes.c_int, [_P, _P]),
+            "orc_node_collides": (ctypes.c_int, [_P, _P, ctypes.c_float, _P, ctypes.c_int]),
             "orc_node_positions": (None, [_P, ctypes.c_int, _P, _P]),
             "orc_residual": (ctypes.c_float, [_P, ctypes.c_int, _P]),
             "orc_calculate_pso": (
@@ -69,26 +77,51 @@ def load():
             "orc_calculate_pso_ex": (
                 ctypes.c_int,
                 [_P, _P, _P, _P, ctypes.c_int64, _P, ctypes.c_int, ctypes.c_float, ctypes.c_float, ctypes.c_float,
-                 ctypes.c_int, ctypes.c_float, ctypes.c_float, _P, ctypes.c_float, _P, _P],
+                 ctypes.c_int, ctypes.c_float, ctypes.c_float, _P, ctypes.c_float, _P, _P, _P, ctypes.c_int],
             ),
             "orc_solve_batch": (
                 ctypes.c_int,
                 [_P, ctypes.c_int, _P, _P, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_float,
                  ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float, _P, _P, _P, _P, _P, ctypes.c_int,
-                 ctypes.c_float, _P, _P],
+                 ctypes.c_float, _P, _P, _P, ctypes.c_int],
             ),
         }
         for name, (res, args) in sig.items():
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
-        assert lib.orc_sizeof_rng() == 48 and lib.orc_sizeof_node() == 88
+        assert lib.orc_sizeof_rng() == 48 and lib.orc_sizeof_node() == 88 and lib.orc_sizeof_box() == 48
         _LIB = lib
     return _LIB
 
 
 def _p(a):
     return None if a is None else a.ctypes.data
+
+
+def _boxes(colliders):
+    """(array or None, count) for a BOX_DTYPE-compatible collider array."""
+    if colliders is None or len(colliders) == 0:
+        return None, 0
+    b = np.ascontiguousarray(colliders)
+    b = b.view(BOX_DTYPE) if b.dtype != BOX_DTYPE else b
+    return b, int(b.shape[0])
+
+
+def make_box(size, pos, quat=(0.0, 0.0, 0.0, 1.0)) -> np.ndarray:
+    """One obj_t: size = (x, y, z) edge lengths, quat = (x, y, z, w)."""
+    b = np.zeros((), dtype=BOX_DTYPE)
+    b["x"], b["y"], b["z"] = size
+    b["pos"] = pos
+    b["quat"] = quat
+    return b
+
+
+def gjk_intersect(a, b) -> bool:
+    """GJKIntersect (src/kernel.cu:532-536) of two obj_t boxes."""
+    a = np.ascontiguousarray(a, dtype=BOX_DTYPE)
+    b = np.ascontiguousarray(b, dtype=BOX_DTYPE)
+    return bool(load().orc_gjk_intersect(a.ctypes.data, b.ctypes.data))
 
 
 def _chain(chain) -> np.ndarray:
@@ -135,12 +168,13 @@ def _f32(x):
 
 
 def fitness(chain, angles, angle_weight=3.0, distance_weight=0.0, positions=None, limit_weight=0.0, soft_lo=None,
-            soft_hi=None) -> np.float32:
+            soft_hi=None, colliders=None) -> np.float32:
     c = _chain(chain)
     a = _f32(angles)
     pos, lo, hi = _f32(positions), _f32(soft_lo), _f32(soft_hi)
+    bx, nb = _boxes(colliders)
     return np.float32(load().orc_fitness_ex(_p(c), c.shape[0], _p(pos), _p(a), angle_weight, distance_weight,
-                                            limit_weight, _p(lo), _p(hi)))
+                                            limit_weight, _p(lo), _p(hi), _p(bx), nb))
 
 
 def residual(chain, angles) -> np.float32:
@@ -151,7 +185,7 @@ def residual(chain, angles) -> np.float32:
 
 def calculate_pso(chain, size: int, randoms: np.ndarray, inertia=0.5, local=0.5, glob=1.25, iterations=15,
                   angle_weight=3.0, distance_weight=0.0, positions=None, limit_weight=0.0, soft_lo=None,
-                  soft_hi=None):
+                  soft_hi=None, colliders=None):
     """One reference solve.  Advances `randoms` in place.
     Returns (result [D], particles [3, D, size], bests [size])."""
     c = _chain(chain)
@@ -161,15 +195,16 @@ def calculate_pso(chain, size: int, randoms: np.ndarray, inertia=0.5, local=0.5,
     res = np.zeros(D, dtype=np.float32)
     pos = None if positions is None else np.ascontiguousarray(positions, dtype=np.float32)
     lo, hi = _f32(soft_lo), _f32(soft_hi)
+    bx, nb = _boxes(colliders)
     load().orc_calculate_pso_ex(_p(parts), _p(pos), _p(bests), _p(randoms), int(size), _p(c), c.shape[0], inertia,
                                 local, glob, int(iterations), angle_weight, distance_weight, _p(res), limit_weight,
-                                _p(lo), _p(hi))
+                                _p(lo), _p(hi), _p(bx), nb)
     return res, parts, bests
 
 
 def solve_batch(chain, targets, start_pose, particles: int, iterations: int, rng: np.ndarray, inertia=0.5,
                 local=0.5, glob=1.25, angle_weight=3.0, distance_weight=0.0, positions=None, threads: int = 0,
-                limit_weight=0.0, soft_lo=None, soft_hi=None):
+                limit_weight=0.0, soft_lo=None, soft_hi=None, colliders=None):
     """B independent reference solves (OpenMP over swarms).  rng: [B*P] states, advanced in place.
     Returns (angles [B, D], fitness [B], residual [B])."""
     c = _chain(chain)
@@ -182,9 +217,10 @@ def solve_batch(chain, targets, start_pose, particles: int, iterations: int, rng
     fit = np.zeros(B, dtype=np.float32)
     res = np.zeros(B, dtype=np.float32)
     lo, hi = _f32(soft_lo), _f32(soft_hi)
+    bx, nb = _boxes(colliders)
     err = load().orc_solve_batch(_p(c), c.shape[0], _p(t), _p(sp), B, int(particles), int(iterations), inertia,
                                  local, glob, angle_weight, distance_weight, _p(pos), _p(rng), _p(ang), _p(fit),
-                                 _p(res), int(threads), limit_weight, _p(lo), _p(hi))
+                                 _p(res), int(threads), limit_weight, _p(lo), _p(hi), _p(bx), nb)
     if err:
         raise RuntimeError(f"orc_solve_batch failed ({err})")
     return ang, fit, res

@@ -44,7 +44,7 @@ def test_compat_symbols_exported():
 
 def test_abi_version_and_strings():
     lib = _abi.load()
-    assert lib.ikpso_abi_version() == 1
+    assert lib.ikpso_abi_version() == 2
     assert lib.ikpso_status_string(0) == b"ok"
     assert lib.ikpso_status_string(2) == b"unsupported configuration"
 
@@ -60,8 +60,9 @@ def test_struct_layouts_match_header():
       printf("%zu %zu %zu %zu %zu %zu %zu\n", offsetof(ikpso_node, position), offsetof(ikpso_node, rotation),
              offsetof(ikpso_node, max_rotation), offsetof(ikpso_node, min_rotation), offsetof(ikpso_node, length),
              offsetof(ikpso_node, target_position), offsetof(ikpso_collider, quat));
-      printf("%zu %zu %zu\n", sizeof(ikpso_solver_desc), offsetof(ikpso_solver_desc, positions),
-             offsetof(ikpso_solver_desc, soft_hi));
+      printf("%zu %zu %zu %zu %zu\n", sizeof(ikpso_solver_desc), offsetof(ikpso_solver_desc, positions),
+             offsetof(ikpso_solver_desc, soft_hi), offsetof(ikpso_solver_desc, colliders),
+             offsetof(ikpso_solver_desc, collider_count));
       return 0; }
     '''
     with tempfile.TemporaryDirectory() as td:
@@ -80,6 +81,8 @@ def test_struct_layouts_match_header():
     d = list(map(int, out[2].split()))
     assert d[0] == ctypes.sizeof(_abi.SolverDesc)
     assert d[1] == _abi.SolverDesc.positions.offset and d[2] == _abi.SolverDesc.soft_hi.offset
+    assert d[3] == _abi.SolverDesc.colliders.offset and d[4] == _abi.SolverDesc.collider_count.offset
+    assert _abi.COLLIDER_DTYPE.fields["quat"][1] == offs[6]
 
 
 def test_validation_without_device_work():
@@ -88,11 +91,13 @@ def test_validation_without_device_work():
     assert lib.ikpso_init_generators_seeded(None, 5, 0, None) == _abi.IKPSO_ERR_INVALID_ARG
     assert lib.ikpso_solver_seed(None, 1, 0, 0, None) == _abi.IKPSO_ERR_INVALID_ARG
     assert lib.ikpso_solve_batch(None, None, None, 1, 1, None, None, None, None) == _abi.IKPSO_ERR_INVALID_ARG
-    # colliders are a not-yet-built term: refused before any device work
+    # a collider count without colliders is refused before any device work
     pso = _abi.PSOConfig(0.5, 0.5, 1.25, 15)
     fit = _abi.FitnessConfig(3.0, 0.0, 0.1)
     assert lib.ikpso_calculate_pso(None, None, None, None, 16, None, 8, pso, fit, None, None, 1, None) == \
-        _abi.IKPSO_ERR_UNSUPPORTED
+        _abi.IKPSO_ERR_INVALID_ARG
+    assert lib.ikpso_calculate_pso(None, None, None, None, 16, None, 8, pso, fit, None, None, -1, None) == \
+        _abi.IKPSO_ERR_INVALID_ARG
     assert lib.ikpso_calculate_pso(None, None, None, None, 0, None, 8, pso, fit, None, None, 0, None) == \
         _abi.IKPSO_ERR_INVALID_ARG
 

@@ -1,0 +1,130 @@
+"""Collider term (src/kernel.cu:104-136): the oracle's GJK restatement
+(oracle/ikpso_gjk.c) pinned against an independent exact test, and the
+collider plumbing on the host side.
+
+The reference holds no fixtures for this branch (it ships with colliderCount
+= 0, src/Main.cpp:18), so the pin is geometric: box-box intersection decided by
+the separating-axis theorem (15 axes, float64) on random oriented boxes, for
+every pair whose SAT margin exceeds 1e-3 (touching pairs are left out -- any
+fp32 algorithm may go either way there).
+"""
+import numpy as np
+import pytest
+
+import ikpso
+
+
+def quat_matrix(q):
+    """The linear map quatRotVec applies (exact for any quaternion)."""
+    x, y, z, w = (float(v) for v in q)
+    r = np.array([x, y, z])
+    k = np.array([[0, -z, y], [z, 0, -x], [-y, x, 0]])
+    return (1 - 2 * (r @ r)) * np.eye(3) + 2 * np.outer(r, r) + 2 * w * k
+
+
+def sat_margin(a, b):
+    """Largest separation over the 15 SAT axes (> 0: disjoint, < 0: overlapping)."""
+    ra, rb = quat_matrix(a["quat"]), quat_matrix(b["quat"])
+    ha = np.array([a["x"], a["y"], a["z"]], float) / 2
+    hb = np.array([b["x"], b["y"], b["z"]], float) / 2
+    t = np.asarray(b["pos"], float) - np.asarray(a["pos"], float)
+    axes = [ra[:, i] for i in range(3)] + [rb[:, i] for i in range(3)]
+    axes += [np.cross(ra[:, i], rb[:, j]) for i in range(3) for j in range(3)]
+    best = -np.inf
+    for ax in axes:
+        n = np.linalg.norm(ax)
+        if n < 1e-6:
+            continue
+        ax = ax / n
+        pa = sum(ha[i] * abs(ra[:, i] @ ax) for i in range(3))
+        pb = sum(hb[i] * abs(rb[:, i] @ ax) for i in range(3))
+        best = max(best, abs(t @ ax) - pa - pb)
+    return best
+
+
+def random_quat(rng):
+    q = rng.normal(size=4)
+    return q / np.linalg.norm(q)
+
+
+def test_gjk_matches_separating_axis_test(oracle):
+    rng = np.random.default_rng(0)
+    checked = 0
+    for _ in range(4000):
+        a = oracle.make_box(rng.uniform(0.05, 1.5, 3), rng.uniform(-3, 3, 3), random_quat(rng))
+        d = rng.normal(size=3)
+        d /= np.linalg.norm(d)
+        b = oracle.make_box(rng.uniform(0.05, 1.5, 3), a["pos"] + d * rng.uniform(0, 2.5), random_quat(rng))
+        m = sat_margin(a, b)
+        if abs(m) < 1e-3:
+            continue
+        assert oracle.gjk_intersect(a, b) == (m < 0), (a, b, m)
+        checked += 1
+    assert checked > 3900
+
+
+def test_gjk_edge_cases(oracle):
+    a = oracle.make_box((1, 1, 1), (0, 0, 0))
+    assert oracle.gjk_intersect(a, a)                                        # coincident
+    assert oracle.gjk_intersect(a, oracle.make_box((0.1, 0.1, 0.1), (0, 0, 0)))  # contained
+    assert not oracle.gjk_intersect(a, oracle.make_box((1, 1, 1), (1.01, 0, 0)))
+    assert oracle.gjk_intersect(a, oracle.make_box((1, 1, 1), (0.99, 0, 0)))
+    assert not oracle.gjk_intersect(a, oracle.make_box((1, 1, 1), (5, 5, 5)))
+    # a degenerate (zero) quaternion: quatInvert2 keeps the copy, rotation maps to 0 -> a point box
+    z = oracle.make_box((1, 1, 1), (0.2, 0, 0), (0, 0, 0, 0))
+    assert oracle.gjk_intersect(a, z)
+
+
+def node_link_boxes(oracle, chain, angles):
+    """The reference's node and link boxes (src/kernel.cu:104-126), float64 from the oracle's matrices."""
+    m = oracle.chain_matrices(chain, angles).reshape(-1, 4, 4)
+    out = []
+    for k in range(1, chain.shape[0]):
+        rot = m[k, :3, :3].astype(np.float64)
+        # quaternion of the rotation (any sign: SAT only needs the matrix)
+        from scipy.spatial.transform import Rotation
+        q = Rotation.from_matrix(rot).as_quat()  # x, y, z, w
+        p = m[k, :3, 3]
+        pp = m[chain[k]["parent_index"], :3, 3]
+        out.append(oracle.make_box((0.2, 0.2, 0.2), p, q))
+        out.append(oracle.make_box((chain[k]["length"], 0.05, 0.05), (p + pp) * 0.5, q))
+    return out
+
+
+def test_fitness_collider_term(oracle):
+    chain = ikpso.reference_scene(reset=True).origin.to_cuda()
+    boxes = ikpso.init_colliders(4)
+    rng = np.random.default_rng(3)
+    hits = misses = 0
+    for _ in range(300):
+        ang = rng.uniform(0, 2 * np.pi, 21).astype(np.float32)
+        f0 = oracle.fitness(chain, ang)
+        f = oracle.fitness(chain, ang, colliders=boxes)
+        margins = [sat_margin(nb, cb) for nb in node_link_boxes(oracle, chain, ang) for cb in boxes]
+        if min(margins) < -1e-3:
+            assert f == np.float32(np.finfo(np.float32).max)
+            hits += 1
+        elif min(margins) > 1e-3:
+            assert f == f0
+            misses += 1
+    assert hits > 30 and misses > 30
+
+
+def test_calculate_pso_with_colliders_avoids_them(oracle):
+    chain = ikpso.reference_scene(reset=True).origin.to_cuda()
+    # colliders 1 and 2 already intersect the reset pose (every particle would
+    # start at FLT_MAX and, with strict improvement, could never move its pbest)
+    boxes = ikpso.init_colliders(4)[[0, 3]]
+    st = oracle.init_generators(128, 0)
+    res, parts, bests = oracle.calculate_pso(chain, 128, st, iterations=30, colliders=boxes)
+    fmax = np.float32(np.finfo(np.float32).max)
+    assert bests.min() < fmax
+    assert oracle.fitness(chain, res, colliders=boxes) < fmax
+
+
+def test_init_colliders_matches_visualiser():
+    c = ikpso.init_colliders(4)
+    assert c.dtype.itemsize == 48 and len(c) == 4
+    assert np.allclose(c["pos"], [[1, 0, 0], [0, 0, -1], [-1, 0, 0], [0, 0, 1]])
+    assert np.allclose(c[1]["quat"], [-0.403, -0.819, 0.273, 0.304])
+    assert np.all(c["x"] == 1) and len(ikpso.init_colliders(0)) == 0

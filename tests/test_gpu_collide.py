@@ -1,0 +1,110 @@
+"""Collider term on the GPU (ikpso_collide.h) vs the oracle's GJK restatement
+(oracle/ikpso_gjk.c), through the C ABI.
+
+Tolerances: the collision decision is integer-like (hit -> FLT_MAX), so in
+REFERENCE arithmetic (the reference's FK operation order on both sides) the
+fitness of every pose and the whole calculatePSO state are compared bit for
+bit.  In FAST arithmetic the node frames differ by FMA rounding (<= 2e-5), so
+decisions may flip only for boxes within that distance of touching: >= 99% of
+decisions must agree and finite fitness values meet the FAST FK tolerance.
+"""
+import numpy as np
+import pytest
+
+import ikpso
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+FMAX = np.float32(np.finfo(np.float32).max)
+
+
+def dev(x):
+    return torch.from_numpy(np.ascontiguousarray(x)).cuda()
+
+
+@pytest.fixture(scope="module")
+def scene_chain():
+    return ikpso.reference_scene(reset=True).origin.to_cuda()
+
+
+def random_colliders(rng, n):
+    c = np.zeros(n, dtype=ikpso.COLLIDER_DTYPE)
+    for i in range(n):
+        q = rng.normal(size=4)
+        c[i]["x"], c[i]["y"], c[i]["z"] = rng.uniform(0.2, 1.2, 3)
+        c[i]["pos"] = rng.uniform(-2.5, 2.5, 3)
+        c[i]["quat"] = q / np.linalg.norm(q)
+    return c
+
+
+@pytest.mark.parametrize("arith", ["reference", "fast"])
+def test_evaluate_with_colliders(oracle, device, scene_chain, arith):
+    rng = np.random.default_rng(11)
+    n = 3000
+    ang = rng.uniform(0, 2 * np.pi, (n, 21)).astype(np.float32)
+    for boxes in (ikpso.init_colliders(4), random_colliders(rng, 3)):
+        s = ikpso.BatchSolver(scene_chain, 64, arith=arith, colliders=boxes)
+        fit = s.evaluate(dev(ang))[0].cpu().numpy()
+        s.close()
+        ofit = np.array([oracle.fitness(scene_chain, a, colliders=boxes) for a in ang], dtype=np.float32)
+        hit, ohit = fit == FMAX, ofit == FMAX
+        assert 0.05 < ohit.mean() < 0.95  # both outcomes exercised
+        if arith == "reference":
+            assert np.array_equal(fit, ofit)
+        else:
+            assert np.mean(hit == ohit) >= 0.99
+            both = ~hit & ~ohit
+            assert np.max(np.abs(fit[both] - ofit[both]) / ofit[both]) < 1e-5
+
+
+def run_compat(chain, P, I, colliders, seed_base=0):
+    D = 3 * (chain.shape[0] - 1)
+    parts = ikpso.particles_tensor(P, D)
+    bests = torch.zeros(P, dtype=torch.float32, device="cuda")
+    r = ikpso.rng_tensor(P)
+    assert ikpso.init_generators_seeded(r, P, seed_base) == 0
+    res = np.zeros(D, dtype=np.float32)
+    st = ikpso.calculate_pso(parts, None, bests, r, P, chain, ikpso.PSOConfig(0.5, 0.5, 1.25, I),
+                             ikpso.FitnessConfig(3.0, 0.0, 0.1), res, colliders, len(colliders))
+    assert st == 0
+    return res, parts.cpu().numpy(), bests.cpu().numpy(), r.cpu().numpy()
+
+
+@pytest.mark.parametrize("kernel,P,I", [("resident", 256, 20), ("streaming", 600, 8)])
+def test_calculate_pso_with_colliders_reference_bitexact(oracle, device, scene_chain, monkeypatch, kernel, P, I):
+    """calculatePSO(..., colliders, colliderCount) with colliders 0 and 3 of
+    initColliders (1 and 2 intersect the reset pose), REFERENCE arithmetic."""
+    monkeypatch.setenv("IKPSO_ARITH", "reference")
+    monkeypatch.setenv("IKPSO_KERNEL", kernel)
+    boxes = ikpso.init_colliders(4)[[0, 3]]
+    res, parts, bests, r = run_compat(scene_chain, P, I, boxes)
+    ostate = oracle.init_generators(P, 0)
+    ores, oparts, obests = oracle.calculate_pso(scene_chain, P, ostate, iterations=I, colliders=boxes)
+    assert np.array_equal(r[:, :6], ostate.view(np.int32).reshape(P, 12)[:, :6])
+    assert np.array_equal(bests, obests) and np.array_equal(parts, oparts) and np.array_equal(res, ores)
+    assert (bests == FMAX).any() and (bests < FMAX).any()
+    assert oracle.fitness(scene_chain, res, colliders=boxes) < FMAX
+
+
+def test_batch_with_colliders_fast(oracle, device):
+    """Batched FAST solve with a collider between the arm and its targets:
+    every swarm's answer is collision-free and its fitness matches the oracle's
+    statistically (tier B)."""
+    wl = ikpso.workload(3)
+    B, P, I = 32, 256, 40
+    boxes = np.concatenate([ikpso.make_collider((0.6, 0.6, 0.6), (0.0, 0.9, -1.6)), ikpso.init_colliders(1)])
+    tg = wl.targets(0, B)
+    s = ikpso.BatchSolver(wl.chain, P, pso=wl.pso, colliders=boxes)
+    s.seed(B)
+    ang, fit, res = (t.cpu().numpy() for t in s.solve(dev(tg), iterations=I))
+    s.close()
+    ostate = oracle.init_generators(B * P, 0)
+    oang, ofit, ores = oracle.solve_batch(wl.chain, tg, None, P, I, ostate, colliders=boxes, threads=8)
+    assert (fit < FMAX).all() and (ofit < FMAX).all()
+    for b in range(B):
+        ch = wl.chain.copy()
+        ch["target_position"][5:8] = tg[b]
+        assert oracle.fitness(ch, ang[b], colliders=boxes) < FMAX
+    assert abs(fit.mean() - ofit.mean()) / ofit.mean() < 0.02
