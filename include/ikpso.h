@@ -121,7 +121,8 @@ ikpso_status ikpso_init_generators_seeded(ikpso_rng_state* randoms, int64_t coun
  *   particles [3][D][size] floats, device: SoA position / velocity / local best
  *             (src/kernel.cu:17-29); overwritten with the final swarm state.
  *   positions [4*J] floats, any: host-computed arm positions, read only when
- *             fit.distance_weight != 0, at slot (k-1)*4 for node k (src/kernel.cu:94-98).
+ *             fit.distance_weight != 0, at slot (k-1)*4 for node k (src/kernel.cu:94-98);
+ *             [4*(J+2)] read at slot (k+1)*4 with IKPSO_POSREF=node_slot (see IKPSO_FLAG_*).
  *   bests     [size] floats, device: final local-best fitness per particle.
  *   randoms   [size] states, device: consumed and advanced (persist across calls).
  *   chain     [node_count] nodes, any.  D = 3*(node_count-1).
@@ -158,8 +159,18 @@ typedef struct ikpso_solver_desc {
     /* Collider term, as calculatePSO's colliders/colliderCount (ABI >= 2). */
     const ikpso_collider* colliders; /* any, [collider_count] or NULL */
     int32_t collider_count;
-    int32_t reserved2;
+    int32_t flags;            /* IKPSO_FLAG_* */
 } ikpso_solver_desc;
+
+/* ikpso_solver_desc.flags (env IKPSO_POSREF=node_slot for ikpso_calculate_pso). */
+enum {
+    /* Distance term with the reference's latent slot bug fixed (opt-in): the
+     * reference reads node k's reference position from positions[(k-1)*4],
+     * which FillPositions (src/Node.h:110-149) filled with node k-2's; with
+     * this flag positions is [4*(J+2)] as FillPositions writes it and node k
+     * reads slot k+1, its own.  Off: bit-compatible with the reference. */
+    IKPSO_FLAG_POSREF_NODE_SLOT = 1
+};
 
 ikpso_status ikpso_solver_create(const ikpso_solver_desc* desc, ikpso_solver** out);
 ikpso_status ikpso_solver_destroy(ikpso_solver* solver);

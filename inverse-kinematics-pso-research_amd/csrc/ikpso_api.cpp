@@ -124,6 +124,9 @@ struct Extras {
     const float* soft_hi = nullptr;
     const ikpso_collider* colliders = nullptr;  // host copy, [collider_count]
     int collider_count = 0;
+    // IKPSO_FLAG_POSREF_NODE_SLOT: positions[] is [4*(J+2)] and node k's
+    // reference position is read from slot k+1 (where FillPositions wrote it)
+    bool posref_node_slot = false;
 };
 
 // Device record of one obj_t collider (ikpso_collide.h): the inverse
@@ -226,7 +229,7 @@ ikpso_status parse_chain(const std::vector<ikpso_node>& nodes, const ikpso_pso_c
             return IKPSO_ERR_INVALID_ARG;
     }
     if (ch.use_posref && ex.positions)
-        for (int i = 0; i < 4 * J; ++i) ch.aux[i] = ex.positions[i];
+        for (int i = 0; i < 4 * J; ++i) ch.aux[i] = ex.positions[i + (ex.posref_node_slot ? 8 : 0)];
     if (ch.use_penalty)
         for (int d = 0; d < 3 * J; ++d) {
             ch.aux[4 * J + d] = ex.soft_lo[d];
@@ -373,8 +376,11 @@ ikpso_status ikpso_calculate_pso(float* particles, const float* positions, float
     std::vector<float> pos;
     Extras ex;
     if (fit.distance_weight != 0.0f && positions) {
-        pos.resize(4 * J);
-        st = fetch_any(pos.data(), positions, sizeof(float) * 4 * J);
+        const char* ps = getenv("IKPSO_POSREF");
+        ex.posref_node_slot = ps && strcmp(ps, "node_slot") == 0;
+        const size_t n = 4 * (size_t)(ex.posref_node_slot ? J + 2 : J);
+        pos.resize(n);
+        st = fetch_any(pos.data(), positions, sizeof(float) * n);
         if (st != IKPSO_OK) return st;
         ex.positions = pos.data();
     }
@@ -446,8 +452,10 @@ ikpso_status ikpso_solver_create(const ikpso_solver_desc* desc, ikpso_solver** o
     std::vector<float> pos, slo, shi;
     Extras ex;
     if (desc->fit.distance_weight != 0.0f && desc->positions) {
-        pos.resize(4 * J);
-        if ((st = fetch_any(pos.data(), desc->positions, sizeof(float) * 4 * J)) != IKPSO_OK) return st;
+        ex.posref_node_slot = (desc->flags & IKPSO_FLAG_POSREF_NODE_SLOT) != 0;
+        const size_t n = 4 * (size_t)(ex.posref_node_slot ? J + 2 : J);
+        pos.resize(n);
+        if ((st = fetch_any(pos.data(), desc->positions, sizeof(float) * n)) != IKPSO_OK) return st;
         ex.positions = pos.data();
     }
     if (desc->limit_weight != 0.0f) {

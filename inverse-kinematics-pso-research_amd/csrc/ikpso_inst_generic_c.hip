@@ -1,5 +1,4 @@
-// ikpso_inst_generic_c.hip -- kernel instantiations (generated layout: one unit per
-// heavy (topology, mode[, family]) so the build parallelises).
+// ikpso_inst_generic_c.hip -- kernel instantiations for generic trees of 9, 10 joints.
 #include "ikpso_topo_impl.h"
 
 namespace ikpso {

@@ -1,10 +1,11 @@
-// ikpso_inst_generic_e.hip -- kernel instantiations (generated layout: one unit per
-// heavy (topology, mode[, family]) so the build parallelises).
+// ikpso_inst_generic_e.hip -- kernel instantiations for generic trees of 13, 14 joints.
 #include "ikpso_topo_impl.h"
 
 namespace ikpso {
 #ifndef IKPSO_EXPERIMENT_REF7_ONLY
-template struct ModeOps<TopoGeneric<16>, IKPSO_ARITH_FAST>;
-template struct ModeOps<TopoGeneric<16>, IKPSO_ARITH_REFERENCE>;
+template struct ModeOps<TopoGeneric<13>, IKPSO_ARITH_FAST>;
+template struct ModeOps<TopoGeneric<13>, IKPSO_ARITH_REFERENCE>;
+template struct ModeOps<TopoGeneric<14>, IKPSO_ARITH_FAST>;
+template struct ModeOps<TopoGeneric<14>, IKPSO_ARITH_REFERENCE>;
 #endif
 }  // namespace ikpso

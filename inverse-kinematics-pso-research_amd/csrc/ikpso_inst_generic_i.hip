@@ -1,0 +1,9 @@
+// ikpso_inst_generic_i.hip -- kernel instantiations for generic trees of 20 joints.
+#include "ikpso_topo_impl.h"
+
+namespace ikpso {
+#ifndef IKPSO_EXPERIMENT_REF7_ONLY
+template struct ModeOps<TopoGeneric<20>, IKPSO_ARITH_FAST>;
+template struct ModeOps<TopoGeneric<20>, IKPSO_ARITH_REFERENCE>;
+#endif
+}  // namespace ikpso

@@ -13,6 +13,8 @@
 //     (randInitKernel, src/utility_kernels.cuh:21-31).
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "ikpso_device.h"
 #include "ikpso_kernels.h"
 #include "ikpso_swarm.h"
@@ -68,12 +70,19 @@ bool chain_supported(const ChainHost& ch)
 
 const char* kernel_name(const ChainHost& ch, bool streaming)
 {
-    const bool spec = ch.topo == TopoKind::Ref7 || (ch.topo == TopoKind::SerialTip && ch.J == 20);
-    if (streaming)
-        return ch.topo == TopoKind::Ref7 ? "swarm_streaming<ref_tree7>"
-                                         : (spec ? "swarm_streaming<serial_tip20>" : "swarm_streaming<generic>");
-    return ch.topo == TopoKind::Ref7 ? "swarm_resident<ref_tree7>"
-                                     : (spec ? "swarm_resident<serial_tip20>" : "swarm_resident<generic>");
+    const char* name = streaming ? "swarm_streaming<generic>" : "swarm_resident<generic>";
+    visit_topology(ch, [&](auto topo) {
+        using T = decltype(topo);
+        if constexpr (std::is_same_v<T, TopoRef7>)
+            name = streaming ? "swarm_streaming<ref_tree7>" : "swarm_resident<ref_tree7>";
+        else if constexpr (std::is_same_v<T, TopoSerialTip<6>>)
+            name = streaming ? "swarm_streaming<serial_tip6>" : "swarm_resident<serial_tip6>";
+        else if constexpr (std::is_same_v<T, TopoSerialTip<7>>)
+            name = streaming ? "swarm_streaming<serial_tip7>" : "swarm_resident<serial_tip7>";
+        else if constexpr (std::is_same_v<T, TopoSerialTip<20>>)
+            name = streaming ? "swarm_streaming<serial_tip20>" : "swarm_resident<serial_tip20>";
+    });
+    return name;
 }
 
 hipError_t launch_resident(const ChainHost& ch, int mode, const SwarmIO& io, hipStream_t stream)

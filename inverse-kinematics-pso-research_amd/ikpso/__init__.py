@@ -11,6 +11,7 @@ from .scene import (RESET_TARGETS, EffectorNode, Node, OriginNode, Scene, Target
                     init_colliders, reference_scene, serial_chain)
 from .solver import (MAIN_FITNESS, MAIN_PSO, BatchSolver, FitnessConfig, PSOConfig, calculate_pso,
                      init_generators, init_generators_seeded, make_collider, particles_tensor, rng_tensor)
+from .dh import DHArm, dh_arm, dh_forward
 from .workloads import Workload, workload
 
 __all__ = [
@@ -18,5 +19,5 @@ __all__ = [
     "IkpsoError", "load", "RESET_TARGETS", "EffectorNode", "Node", "OriginNode", "Scene", "TargetNode",
     "check_distance", "reference_scene", "serial_chain", "MAIN_FITNESS", "MAIN_PSO", "BatchSolver",
     "FitnessConfig", "PSOConfig", "calculate_pso", "init_generators", "init_generators_seeded",
-    "particles_tensor", "rng_tensor", "Workload", "workload",
+    "particles_tensor", "rng_tensor", "Workload", "workload", "DHArm", "dh_arm", "dh_forward",
 ]

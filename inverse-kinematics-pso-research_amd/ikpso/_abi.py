@@ -73,6 +73,8 @@ assert COLLIDER_DTYPE.itemsize == 48
 
 ABI_VERSION = 2
 
+FLAG_POSREF_NODE_SLOT = 1  # IKPSO_FLAG_POSREF_NODE_SLOT
+
 
 # ------------------------------------------------------------ ctypes structs
 class PSOConfig(ctypes.Structure):
@@ -112,7 +114,7 @@ class SolverDesc(ctypes.Structure):
         ("soft_hi", ctypes.c_void_p),
         ("colliders", ctypes.c_void_p),
         ("collider_count", ctypes.c_int32),
-        ("reserved2", ctypes.c_int32),
+        ("flags", ctypes.c_int32),
     ]
 
 

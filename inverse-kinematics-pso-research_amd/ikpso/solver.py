@@ -170,7 +170,8 @@ class BatchSolver:
 
     def __init__(self, chain: np.ndarray, particles: int, pso: PSOConfig = MAIN_PSO,
                  fit: FitnessConfig = MAIN_FITNESS, arith: str = "fast", positions=None,
-                 limit_weight: float = 0.0, soft_lo=None, soft_hi=None, kernel: str = "auto", colliders=None):
+                 limit_weight: float = 0.0, soft_lo=None, soft_hi=None, kernel: str = "auto", colliders=None,
+                 posref_node_slot: bool = False):
         self._lib = _abi.load()
         if chain.dtype != NODE_DTYPE:
             raise TypeError("chain must be an ikpso NODE_DTYPE array")
@@ -192,6 +193,7 @@ class BatchSolver:
         desc.limit_weight = float(limit_weight)
         desc.soft_lo = _any_ptr(None if soft_lo is None else np.asarray(soft_lo, np.float32), keep)
         desc.soft_hi = _any_ptr(None if soft_hi is None else np.asarray(soft_hi, np.float32), keep)
+        desc.flags = _abi.FLAG_POSREF_NODE_SLOT if posref_node_slot else 0
         if colliders is not None and len(colliders):
             boxes = _colliders(colliders)
             desc.colliders = _any_ptr(boxes, keep)
