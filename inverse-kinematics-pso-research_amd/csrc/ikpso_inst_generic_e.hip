@@ -2,7 +2,7 @@
 #include "ikpso_topo_impl.h"
 
 namespace ikpso {
-#ifndef IKPSO_EXPERIMENT_REF7_ONLY
+#if IKPSO_WITH_OTHERS
 template struct ModeOps<TopoGeneric<13>, IKPSO_ARITH_FAST>;
 template struct ModeOps<TopoGeneric<13>, IKPSO_ARITH_REFERENCE>;
 template struct ModeOps<TopoGeneric<14>, IKPSO_ARITH_FAST>;

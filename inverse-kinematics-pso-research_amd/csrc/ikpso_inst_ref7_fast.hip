@@ -3,5 +3,7 @@
 #include "ikpso_topo_impl.h"
 
 namespace ikpso {
+#if IKPSO_WITH_REF7
 template struct ModeOps<TopoRef7, IKPSO_ARITH_FAST>;
+#endif
 }  // namespace ikpso

@@ -3,7 +3,7 @@
 #include "ikpso_topo_impl.h"
 
 namespace ikpso {
-#ifndef IKPSO_EXPERIMENT_REF7_ONLY
+#if IKPSO_WITH_SERIAL20
 template hipError_t ModeOps<TopoSerialTip<20>, IKPSO_ARITH_FAST>::resident(const ChainHost&, const SwarmIO&, int, hipStream_t);
 #endif
 }  // namespace ikpso

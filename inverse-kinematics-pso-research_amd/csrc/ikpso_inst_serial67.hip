@@ -3,7 +3,7 @@
 #include "ikpso_topo_impl.h"
 
 namespace ikpso {
-#ifndef IKPSO_EXPERIMENT_REF7_ONLY
+#if IKPSO_WITH_OTHERS
 template struct ModeOps<TopoSerialTip<6>, IKPSO_ARITH_FAST>;
 template struct ModeOps<TopoSerialTip<6>, IKPSO_ARITH_REFERENCE>;
 template struct ModeOps<TopoSerialTip<7>, IKPSO_ARITH_FAST>;

@@ -12,6 +12,21 @@
 #include "ikpso_collide.h"
 #include "ikpso_params.h"
 
+// Experiment builds (tools/build_variants.sh) compile a subset of topologies.
+#if defined(IKPSO_EXPERIMENT_REF7_ONLY)
+#define IKPSO_WITH_REF7 1
+#define IKPSO_WITH_SERIAL20 0
+#define IKPSO_WITH_OTHERS 0
+#elif defined(IKPSO_EXPERIMENT_SERIAL20_ONLY)
+#define IKPSO_WITH_REF7 0
+#define IKPSO_WITH_SERIAL20 1
+#define IKPSO_WITH_OTHERS 0
+#else
+#define IKPSO_WITH_REF7 1
+#define IKPSO_WITH_SERIAL20 1
+#define IKPSO_WITH_OTHERS 1
+#endif
+
 namespace ikpso {
 
 // Ref7: the reference scene's tree with effectors on nodes 5..7; SerialTip:

@@ -19,6 +19,13 @@
 #include "ikpso_kernels.h"
 #include "ikpso_swarm.h"
 
+#ifndef IKPSO_STREAM_AHEAD
+#define IKPSO_STREAM_AHEAD 2
+#endif
+#ifndef IKPSO_STREAM_PBEST
+#define IKPSO_STREAM_PBEST 1
+#endif
+
 namespace ikpso {
 
 // Resolve the swarm's global best as of the end of launch t-1: reduce the C
@@ -159,32 +166,38 @@ __global__ void __launch_bounds__(kStreamChunk) k_stream_step(const ChainConsts<
         // while only a handful of angles are live at a time.
         const PsoCoef coef = pso_coef(cc);
         FitnessAcc<Topo, MODE, TERMS> acc(cc);
-        // Loads are software-pipelined one node ahead and every node ends in a
-        // scheduling barrier: left alone, the compiler hoists all 9J loads to
-        // the top (256 VGPRs, one wave per SIMD, latency-bound).
-        float nx[3], nv[3], npb[3];
+        // Loads are software-pipelined AHEAD nodes ahead (a ring of AHEAD+1
+        // node slots in registers, indices resolved at compile time) and every
+        // node ends in a scheduling barrier: left alone, the compiler hoists
+        // all 9J loads to the top (256 VGPRs, one wave per SIMD,
+        // latency-bound); one node ahead leaves HBM latency exposed.
+        constexpr int AHEAD = (IKPSO_STREAM_AHEAD < J) ? IKPSO_STREAM_AHEAD : J;
+        float ring[AHEAD + 1][9];
 #pragma unroll
-        for (int ax = 0; ax < 3; ++ax) {
-            nx[ax] = pl.ld(0, ax);
-            nv[ax] = pl.ld(1, ax);
-            npb[ax] = pl.ld(2, ax);
-        }
+        for (int s = 0; s < AHEAD; ++s)
+#pragma unroll
+            for (int ax = 0; ax < 3; ++ax) {
+                ring[s][ax] = pl.ld(0, 3 * s + ax);
+                ring[s][3 + ax] = pl.ld(1, 3 * s + ax);
+                ring[s][6 + ax] = pl.ld(2, 3 * s + ax);
+            }
 #pragma unroll
         for (int kn = 1; kn <= J; ++kn) {
             float cx[3], cv[3], cpb[3];
+            const int cs = (kn - 1) % (AHEAD + 1);
 #pragma unroll
             for (int ax = 0; ax < 3; ++ax) {
-                cx[ax] = nx[ax];
-                cv[ax] = nv[ax];
-                cpb[ax] = npb[ax];
+                cx[ax] = ring[cs][ax];
+                cv[ax] = ring[cs][3 + ax];
+                cpb[ax] = ring[cs][6 + ax];
             }
-            if (kn < J) {
+            if (kn - 1 + AHEAD < J) {  // node kn + AHEAD (0-based kn - 1 + AHEAD)
+                const int nn = kn - 1 + AHEAD, ns = nn % (AHEAD + 1);
 #pragma unroll
                 for (int ax = 0; ax < 3; ++ax) {
-                    const int d = 3 * kn + ax;
-                    nx[ax] = pl.ld(0, d);
-                    nv[ax] = pl.ld(1, d);
-                    npb[ax] = pl.ld(2, d);
+                    ring[ns][ax] = pl.ld(0, 3 * nn + ax);
+                    ring[ns][3 + ax] = pl.ld(1, 3 * nn + ax);
+                    ring[ns][6 + ax] = pl.ld(2, 3 * nn + ax);
                 }
             }
 #pragma unroll
@@ -203,12 +216,30 @@ __global__ void __launch_bounds__(kStreamChunk) k_stream_step(const ChainConsts<
         }
         // updateLocalBests (src/kernel.cu:202-221)
         const float f = acc.finish(cc);
+#if IKPSO_STREAM_PBEST == 0
         if (f < pbf) {
             pbf = f;
             io.pbf[b * P + i] = f;
 #pragma unroll
             for (int d = 0; d < D; ++d) pl.st(2, d, pl.ld(0, d));  // this lane's own stores
         }
+#else
+        // Whole-line stores only: a store covering part of a 128-B line makes
+        // the memory side fetch the line first.  A wave with no improving lane
+        // writes nothing; otherwise every lane rewrites its local best (its new
+        // position, or the old value read back -- an L2 hit, read by the update
+        // above).
+        const bool imp = f < pbf;
+        pbf = imp ? f : pbf;
+        if (__builtin_amdgcn_ballot_w64(imp)) {
+            io.pbf[b * P + i] = pbf;
+#pragma unroll
+            for (int d = 0; d < D; ++d) {
+                const float xn = pl.ld(0, d), po = pl.ld(2, d);
+                pl.st(2, d, imp ? xn : po);
+            }
+        }
+#endif
         io.rng[0 * n + k] = rng.d;
         io.rng[1 * n + k] = rng.v0;
         io.rng[2 * n + k] = rng.v1;

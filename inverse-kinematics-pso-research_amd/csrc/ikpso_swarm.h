@@ -150,31 +150,38 @@ inline bool visit_topology(const ChainHost& ch, F&& f)
 {
     switch (ch.topo) {
     case TopoKind::Ref7:
+#if IKPSO_WITH_REF7
         f(TopoRef7{});
         return true;
-#ifndef IKPSO_EXPERIMENT_REF7_ONLY
+#else
+        break;
+#endif
     case TopoKind::SerialTip:
         switch (ch.J) {  // common arm lengths (6- and 7-joint DH arms) and BASELINE config 5
+#if IKPSO_WITH_OTHERS
         case 6: f(TopoSerialTip<6>{}); return true;
         case 7: f(TopoSerialTip<7>{}); return true;
+#endif
+#if IKPSO_WITH_SERIAL20
         case 20: f(TopoSerialTip<20>{}); return true;
+#endif
         default: break;
         }
-        [[fallthrough]];
+        break;
     case TopoKind::Generic:
-        switch (ch.J) {
+        break;
+    }
+#if IKPSO_WITH_OTHERS
+    switch (ch.J) {  // any tree: runtime parent indices
 #define IKPSO_G(n) \
     case n: f(TopoGeneric<n>{}); return true;
-            IKPSO_G(1) IKPSO_G(2) IKPSO_G(3) IKPSO_G(4) IKPSO_G(5) IKPSO_G(6) IKPSO_G(7) IKPSO_G(8) IKPSO_G(9)
-                IKPSO_G(10) IKPSO_G(11) IKPSO_G(12) IKPSO_G(13) IKPSO_G(14) IKPSO_G(15) IKPSO_G(16) IKPSO_G(17)
-                    IKPSO_G(18) IKPSO_G(19) IKPSO_G(20)
+        IKPSO_G(1) IKPSO_G(2) IKPSO_G(3) IKPSO_G(4) IKPSO_G(5) IKPSO_G(6) IKPSO_G(7) IKPSO_G(8) IKPSO_G(9)
+            IKPSO_G(10) IKPSO_G(11) IKPSO_G(12) IKPSO_G(13) IKPSO_G(14) IKPSO_G(15) IKPSO_G(16) IKPSO_G(17)
+                IKPSO_G(18) IKPSO_G(19) IKPSO_G(20)
 #undef IKPSO_G
-        default: return false;
-        }
-#else
-    default: return false;
-#endif
+    default: break;
     }
+#endif
     return false;
 }
 

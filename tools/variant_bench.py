@@ -33,26 +33,35 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=500)
     ap.add_argument("--arith", default="fast")
+    ap.add_argument("--config", type=int, default=3, choices=[3, 5])
     a = ap.parse_args()
-    wl = ikpso.workload(3)
-    P, I, B = 1024, a.iters, a.swarms
+    wl = ikpso.workload(a.config)
+    P, I, B = wl.particles, a.iters, a.swarms
+    D = 3 * (wl.chain.shape[0] - 1)
     tg = torch.from_numpy(wl.targets(0, B)).cuda()
-    outs = [torch.empty((B, 21), device="cuda"), torch.empty(B, device="cuda"), torch.empty(B, device="cuda")]
+    outs = [torch.empty((B, D), device="cuda"), torch.empty(B, device="cuda"), torch.empty(B, device="cuda")]
     solvers = []
     for p in a.libs:
         lib = open_lib(p)
         desc = _abi.SolverDesc()
         chain = np.ascontiguousarray(wl.chain)
         desc.chain = chain.ctypes.data
-        desc.node_count = 8
+        desc.node_count = chain.shape[0]
         desc.particles = P
         desc.pso = _abi.PSOConfig(0.5, 0.5, 1.25, I)
         desc.fit = _abi.FitnessConfig(3.0, 0.0, 0.1)
         desc.arith = 0 if a.arith == "fast" else 1
+        keep = []
+        if wl.limit_weight:
+            lo = np.ascontiguousarray(wl.soft_lo, np.float32)
+            hi = np.ascontiguousarray(wl.soft_hi, np.float32)
+            keep += [lo, hi]
+            desc.limit_weight = wl.limit_weight
+            desc.soft_lo, desc.soft_hi = lo.ctypes.data, hi.ctypes.data
         h = ctypes.c_void_p()
         assert lib.ikpso_solver_create(ctypes.byref(desc), ctypes.byref(h)) == 0
         assert lib.ikpso_solver_seed(h, B, 0, 0, None) == 0
-        solvers.append((p, lib, h, chain))
+        solvers.append((p, lib, h, (chain, keep)))
     times = {p: [] for p in a.libs}
     results = {}
     for r in range(a.rounds + 1):
