@@ -94,9 +94,12 @@ typedef struct ikpso_collider {
 
 /* Kernel family (ikpso_solver_desc.kernel; env IKPSO_KERNEL for ikpso_calculate_pso). */
 enum {
-    IKPSO_KERNEL_AUTO = 0,      /* resident when the swarm fits one workgroup, else streaming */
+    IKPSO_KERNEL_AUTO = 0,      /* resident when the swarm fits one workgroup, else cooperative, else streaming */
     IKPSO_KERNEL_RESIDENT = 1,  /* one workgroup per swarm, state on chip, one launch per batch */
-    IKPSO_KERNEL_STREAMING = 2  /* state in HBM, one launch per iteration, any swarm size */
+    IKPSO_KERNEL_STREAMING = 2, /* state in HBM, one launch per iteration, any swarm size */
+    IKPSO_KERNEL_COOP = 3       /* one swarm over G co-resident workgroups (G CUs), state on chip, one
+                                   launch per batch; AUTO picks it for swarms above one workgroup when
+                                   the chain has a specialised kernel and G <= CUs / 8 */
 };
 
 /* Arithmetic mode of the device kernels. */

@@ -300,16 +300,51 @@ int env_kernel()
     if (!e) return IKPSO_KERNEL_AUTO;
     if (strcmp(e, "resident") == 0) return IKPSO_KERNEL_RESIDENT;
     if (strcmp(e, "streaming") == 0) return IKPSO_KERNEL_STREAMING;
+    if (strcmp(e, "coop") == 0) return IKPSO_KERNEL_COOP;
     return IKPSO_KERNEL_AUTO;
 }
 
+// Cooperative launch plan for swarms of P particles: G workgroups per swarm,
+// NG concurrent groups (a multiple of 8 for the XCD-aware membership, at most
+// one workgroup per CU, at most ceil8(B) groups).  False if infeasible.
+bool coop_plan(const ChainHost& ch, int mode, int P, int64_t B, int* G, int* NG)
+{
+    CoopGeometry geo;
+    if (!coop_geometry(ch, mode, &geo)) return false;
+    const int g = (P + geo.threads - 1) / geo.threads;
+    int ng = (geo.cus * geo.blocks_per_cu / g) & ~7;
+    if (g > 64 || ng < 8) return false;
+    const int64_t want = ((B + 7) / 8) * 8;
+    if (want < ng) ng = (int)want;
+    *G = g;
+    *NG = ng;
+    return true;
+}
+
+// Point the coop fields of `io` into workspace `ws` (coop_workspace_bytes) and
+// clear the counters and the error flag.
+hipError_t carve_coop(SwarmIO& io, void* ws, int G, int NG, int D, hipStream_t s)
+{
+    Carver cv{static_cast<char*>(ws)};
+    io.coop_counter = cv.take<uint32_t>((size_t)NG * kCoopCounterStride);
+    io.coop_error = cv.take<int32_t>(1);
+    io.coop_slots = cv.take<float>((size_t)NG * 2 * G * kCoopSlot(D));
+    io.coop_g = G;
+    io.coop_ng = NG;
+    const size_t zero = reinterpret_cast<char*>(io.coop_slots) - static_cast<char*>(ws);
+    return hipMemsetAsync(ws, 0, zero, s);
+}
+
 // Resolve the kernel family for a chain and swarm size; -1 if impossible.
-int pick_kernel(const ChainHost& ch, int P, int requested)
+int pick_kernel(const ChainHost& ch, int mode, int P, int requested)
 {
     const bool fits = P <= resident_max_threads(ch);
+    int G, NG;
+    const bool coop = coop_plan(ch, mode, P, 1, &G, &NG);
     if (requested == IKPSO_KERNEL_RESIDENT) return fits ? IKPSO_KERNEL_RESIDENT : -1;
     if (requested == IKPSO_KERNEL_STREAMING) return IKPSO_KERNEL_STREAMING;
-    return fits ? IKPSO_KERNEL_RESIDENT : IKPSO_KERNEL_STREAMING;
+    if (requested == IKPSO_KERNEL_COOP) return coop ? IKPSO_KERNEL_COOP : -1;
+    return fits ? IKPSO_KERNEL_RESIDENT : (coop ? IKPSO_KERNEL_COOP : IKPSO_KERNEL_STREAMING);
 }
 
 }  // namespace
@@ -394,12 +429,14 @@ ikpso_status ikpso_calculate_pso(float* particles, const float* positions, float
     ChainHost ch;
     st = parse_chain(nodes, pso, fit, ex, ch);
     if (st != IKPSO_OK) return st;
-    const int family = pick_kernel(ch, size, env_kernel());
-    if (family < 0) return IKPSO_ERR_UNSUPPORTED;
     // The reference-compatible entry has no mode argument; IKPSO_ARITH=reference
     // selects the reference's operation order (parity runs).
     const char* env = getenv("IKPSO_ARITH");
     const int mode = (env && strcmp(env, "reference") == 0) ? IKPSO_ARITH_REFERENCE : IKPSO_ARITH_FAST;
+    const int family = pick_kernel(ch, mode, size, env_kernel());
+    if (family < 0) return IKPSO_ERR_UNSUPPORTED;
+    int cg = 0, cng = 0;
+    if (family == IKPSO_KERNEL_COOP && !coop_plan(ch, mode, size, 1, &cg, &cng)) return IKPSO_ERR_UNSUPPORTED;
 
     std::lock_guard<std::mutex> lk(g_scratch_mu);
     // device scratch: [result D | aux (64-float aligned) | streaming workspace];
@@ -407,7 +444,9 @@ ikpso_status ikpso_calculate_pso(float* particles, const float* positions, float
     // `ch.aux` outlives every use
     const size_t aux_at = ((size_t)D + 63) & ~size_t(63);
     const size_t head = sizeof(float) * (aux_at + ch.aux.size());
-    const size_t ws = family == IKPSO_KERNEL_STREAMING ? stream_workspace_bytes(1, size, D, false) : 0;
+    const size_t ws = family == IKPSO_KERNEL_STREAMING ? stream_workspace_bytes(1, size, D, false)
+                      : family == IKPSO_KERNEL_COOP    ? coop_workspace_bytes(cng, cg, D)
+                                                       : 0;
     float* dres = nullptr;
     st = scratch(((head + 255) & ~size_t(255)) + ws, &dres);
     if (st != IKPSO_OK) return st;
@@ -424,6 +463,23 @@ ikpso_status ikpso_calculate_pso(float* particles, const float* positions, float
         io.iterations = pso.iterations;
         io.num_swarms = 1;
         IKPSO_HIP(launch_resident(ch, mode, io, s));
+    } else if (family == IKPSO_KERNEL_COOP) {
+        SwarmIO io{};
+        io.rng = randoms;
+        io.out_angles = dres;
+        io.dump_particles = particles;
+        io.dump_bests = bests;
+        io.P = size;
+        io.iterations = pso.iterations;
+        io.num_swarms = 1;
+        IKPSO_HIP(carve_coop(io, reinterpret_cast<char*>(dres) + ((head + 255) & ~size_t(255)), cg, cng, D, s));
+        IKPSO_HIP(launch_coop(ch, mode, io, s));
+        int32_t err = 0;
+        IKPSO_HIP(hipMemcpyAsync(result, dres, sizeof(float) * D, hipMemcpyDefault, s));
+        IKPSO_HIP(hipMemcpyAsync(&err, io.coop_error, sizeof(err), hipMemcpyDeviceToHost, s));
+        IKPSO_HIP(hipStreamSynchronize(s));
+        if (err) return hip_status(hipErrorLaunchTimeOut);
+        return IKPSO_OK;
     } else {
         StreamIO io{};
         carve_stream(io, reinterpret_cast<char*>(dres) + ((head + 255) & ~size_t(255)), 1, size, D, false);
@@ -497,11 +553,12 @@ ikpso_status ikpso_solver_create(const ikpso_solver_desc* desc, ikpso_solver** o
         }
         s->chain.aux_dev = s->aux;
     }
-    s->family = pick_kernel(s->chain, s->P, desc->kernel);
-    if (s->family < 0 || desc->kernel < IKPSO_KERNEL_AUTO || desc->kernel > IKPSO_KERNEL_STREAMING) {
+    s->family = pick_kernel(s->chain, s->mode, s->P, desc->kernel);
+    if (s->family < 0 || desc->kernel < IKPSO_KERNEL_AUTO || desc->kernel > IKPSO_KERNEL_COOP) {
         (void)hipFree(s->aux);
         delete s;
-        return desc->kernel == IKPSO_KERNEL_RESIDENT ? IKPSO_ERR_UNSUPPORTED : IKPSO_ERR_INVALID_ARG;
+        return (desc->kernel == IKPSO_KERNEL_RESIDENT || desc->kernel == IKPSO_KERNEL_COOP) ? IKPSO_ERR_UNSUPPORTED
+                                                                                              : IKPSO_ERR_INVALID_ARG;
     }
     *out = s;
     return IKPSO_OK;
@@ -558,6 +615,31 @@ ikpso_status ikpso_solve_batch(ikpso_solver* s, const float* targets, const floa
         return IKPSO_OK;
     }
     const int D = 3 * s->chain.J;
+    if (s->family == IKPSO_KERNEL_COOP) {
+        int G, NG;
+        if (!coop_plan(s->chain, s->mode, s->P, num_swarms, &G, &NG)) return IKPSO_ERR_UNSUPPORTED;
+        const size_t need = coop_workspace_bytes(NG, G, D);
+        if (need > s->ws_bytes) {
+            if (s->ws) IKPSO_HIP(hipFree(s->ws));
+            s->ws = nullptr;
+            s->ws_bytes = 0;
+            IKPSO_HIP(hipMalloc(&s->ws, need));
+            s->ws_bytes = need;
+        }
+        SwarmIO io{};
+        io.targets = targets;
+        io.start_pose = start_pose;
+        io.rng = s->rng;
+        io.out_angles = out_angles;
+        io.out_fitness = out_fitness;
+        io.out_residual = out_residual;
+        io.P = s->P;
+        io.iterations = iterations;
+        io.num_swarms = num_swarms;
+        IKPSO_HIP(carve_coop(io, s->ws, G, NG, D, hs));
+        IKPSO_HIP(launch_coop(s->chain, s->mode, io, hs));
+        return IKPSO_OK;
+    }
     const size_t need = stream_workspace_bytes(num_swarms, s->P, D, true);
     if (need > s->ws_bytes) {
         if (s->ws) IKPSO_HIP(hipFree(s->ws));  // hipFree synchronises the device
@@ -591,7 +673,7 @@ int ikpso_solver_dof(const ikpso_solver* s) { return s ? 3 * s->chain.J : 0; }
 int ikpso_solver_effectors(const ikpso_solver* s) { return s ? s->chain.E : 0; }
 const char* ikpso_solver_kernel_name(const ikpso_solver* s)
 {
-    return s ? kernel_name(s->chain, s->family == IKPSO_KERNEL_STREAMING) : "";
+    return s ? kernel_name(s->chain, s->family) : "";
 }
 
 }  // extern "C"

@@ -1,0 +1,260 @@
+// ikpso_coop.h -- cooperative resident swarm kernel: one swarm spread over G
+// co-resident workgroups (G CUs), state on chip for the whole solve.
+//
+// For swarms larger than one workgroup (BASELINE config 5: 4096 particles of a
+// 60-angle chain; the visualiser's N = 16384) the streaming kernels move
+// x, v and the local bests through HBM every iteration (12·D bytes per
+// particle-update: HBM-bound).  Here every workgroup keeps its chunk of
+// BLOCK particles resident exactly as k_swarm_resident does (x, v, generator
+// state in VGPRs, local bests in LDS) and the G chunks of a swarm meet once
+// per iteration to form the swarm's argmin (thrust::min_element +
+// `globalMin > currentGlobalMin`, src/kernel.cu:297-323):
+//
+//   each chunk: local argmin (first minimum) -> wave 0 publishes {key, index,
+//   winner's local best} to slot [exchange & 1][chunk] with write-through
+//   (sc1) stores -> s_waitcnt vmcnt(0) -> one agent-scope atomic add on the
+//   group's arrival counter -> lane 0 polls the counter (sc1 loads, s_sleep)
+//   until all G chunks of this exchange have arrived -> wave 0 reduces the G
+//   keys in chunk order (ties keep the lowest chunk = lowest particle index)
+//   and, on strict improvement, copies the winner's vector into LDS ->
+//   workgroup barrier.
+//
+// This is the hand-off of MI355X_MICROARCH.md's first table row (one storing
+// wave signals after its own vmcnt wait; sc1 stores and loads on both sides;
+// one workgroup per CU; hipMalloc'd memory), so no L2 write-back/invalidate
+// fence is needed.  Slots are double-buffered by exchange parity: a chunk
+// rewrites parity p only after the wait of the previous exchange, by which
+// time every chunk has read parity p.  Workgroup b sits on XCD b % 8; the G
+// chunks of a group share an XCD (speed only, never correctness).  Waits are
+// bounded: a timed-out wait sets io.coop_error and the kernel drains.
+// Residency is checked at launch (hipLaunchCooperativeKernel).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "ikpso_resident.h"
+
+namespace ikpso {
+
+constexpr uint32_t kCoopSpinLimit = 1u << 22;
+
+__device__ __forceinline__ void st_sc1(float* p, float v)
+{
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float ld_sc1(const float* p)
+{
+    return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t ld_sc1(const uint32_t* p)
+{
+    return __hip_atomic_load(const_cast<uint32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Per-workgroup bookkeeping in LDS, read at its points of use: held in SGPRs
+// across the iteration loop it pushes the chain constants out of the scalar
+// file and the resulting spills cost VGPRs (the resident kernel's rule, see
+// SwarmShared).
+template <int J>
+struct CoopShared {
+    uint32_t gkey;      // the swarm's global-best key (uniform copy for every wave)
+    int32_t abort;      // a group wait timed out: drain
+    int32_t G, member;  // chunks per swarm, this workgroup's chunk
+    uint32_t e;         // exchanges of this group so far (identical in every member)
+    int32_t pad_;
+    int64_t b;          // current swarm
+    uint32_t* counter;  // the group's arrival counter
+    float* slots;       // the group's [2][G] published records
+};
+
+// Exchange `e` of a group: publish this chunk's local argmin, wait for the G
+// chunks, reduce; returns the group-wide minimum key of this exchange (uniform)
+// and leaves the winner's local best in sh.g when it improves on `gkey` (or
+// always when `force`).  Called by every wave; wave 0 does the global work.
+template <int J, int BLOCK>
+__device__ __forceinline__ void coop_exchange(SwarmShared<J>& sh, CoopShared<J>& cs, const float* s_pb,
+                                              uint32_t local_key, int32_t* error, bool force)
+{
+    constexpr int D = 3 * J;
+    constexpr int SLOT = kCoopSlot(D);
+    static_assert(D + 2 <= 64, "wave 0 publishes the record in one store instruction");
+    int lidx;
+    const uint32_t lmin = swarm_argmin<J>(sh, 0, local_key, &lidx);  // one workgroup barrier inside
+    if (wave_id() == 0) {
+        compiler_fence();
+        const int G = cs.G, member = cs.member;
+        const uint32_t e = cs.e;
+        uint32_t* counter = cs.counter;
+        float* slots = cs.slots;
+        const int lane = lane_id_here();
+        float* base = slots + (size_t)(e & 1) * G * SLOT;
+        float* mine = base + (size_t)member * SLOT;
+        // lanes 0..D-1: the winner's local best; lane D: key; lane D+1: global index
+        if (lane < D) st_sc1(mine + 2 + lane, s_pb[lane * BLOCK + lidx]);
+        if (lane == D) st_sc1(mine, __uint_as_float(lmin));
+        if (lane == D + 1) st_sc1(mine + 1, __int_as_float(member * BLOCK + lidx));
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const uint32_t target = (uint32_t)G * (e + 1);
+        int timed_out = 0;
+        if (lane == 0) {
+            __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            uint32_t n = 0;
+            while (ld_sc1(counter) < target) {
+                __builtin_amdgcn_s_sleep(2);
+                if (++n > kCoopSpinLimit) {
+                    timed_out = 1;
+                    break;
+                }
+            }
+        }
+        timed_out = __builtin_amdgcn_readfirstlane(timed_out);  // lane 0's verdict
+        asm volatile("" ::: "memory");
+        // the G chunk keys, in chunk order (lanes 0..G-1; G <= 64)
+        const uint32_t k = lane < G ? __float_as_uint(ld_sc1(base + (size_t)lane * SLOT)) : 0xFFFFFFFFu;
+        const uint32_t gmin = wave_min_u32(k);
+        const int wj = wave_first_lane_eq(k, gmin);
+        const uint32_t cur = cs.gkey;
+        if (force || gmin < cur) {  // uniform within wave 0
+            if (lane < D) sh.g[lane] = ld_sc1(base + (size_t)wj * SLOT + 2 + lane);
+            if (lane == 0) cs.gkey = gmin;
+        }
+        if (lane == 0) {
+            cs.e = e + 1;
+            if (timed_out) {
+                cs.abort = 1;
+                __hip_atomic_store(error, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+    }
+    __syncthreads();
+}
+
+template <class Topo, int MODE, int TERMS>
+__global__ void __launch_bounds__(kCoopThreads<Topo::J>(), kCoopThreads<Topo::J>() / 256)
+    k_swarm_coop(const ChainConsts<Topo::J> cc, const SwarmIO io)
+{
+    constexpr int J = Topo::J;
+    constexpr int D = 3 * J;
+    constexpr int BLOCK = kCoopThreads<J>();
+    const int tid = threadIdx.x;
+    const int P = io.P;
+
+    __shared__ SwarmShared<J> sh;
+    __shared__ CoopShared<J> cs;
+    // local bests [d][lane]; padded to > 80 KiB so a CU never holds two
+    // workgroups (the launch geometry assumes one per CU)
+    constexpr int kPb = (D * BLOCK * 4 > 82 * 1024) ? D * BLOCK : 82 * 1024 / 4;
+    __shared__ float s_pb[kPb];
+    if (tid == 0) {
+        // XCD-aware group membership: workgroups b, b+8, b+16, ... share an XCD
+        const int G = io.coop_g;
+        const int xcd = blockIdx.x & 7, pos = blockIdx.x >> 3;
+        const int group = (pos / G) * 8 + xcd;
+        cs.G = G;
+        cs.member = pos % G;
+        cs.e = 0;
+        cs.abort = 0;
+        cs.b = group;
+        cs.counter = io.coop_counter + (size_t)group * kCoopCounterStride;
+        cs.slots = io.coop_slots + (size_t)group * 2 * G * kCoopSlot(D);
+    }
+    __syncthreads();
+    const PsoCoef coef = pso_coef(cc);
+
+    for (;;) {
+        compiler_fence();
+        const int64_t b = cs.b;
+        if (b >= io.num_swarms) break;
+        const int i = cs.member * BLOCK + tid;  // particle index within the swarm
+        stage_swarm_inputs<J>(cc, io.targets, io.start_pose, b, sh);
+        Xorwow rng{0, 0, 0, 0, 0, 0};
+        if (i < P) load_rng(rng, io.rng + b * P + i);
+        if (tid == 0) cs.gkey = 0xFFFFFFFFu;
+        __syncthreads();
+
+        // initParticlesKernel + initLocalBests (src/kernel.cu:191-266)
+        float x[D], v[D];
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            x[d] = sh.rest[d];
+            v[d] = __builtin_fmaf(rng.uniform(), 2.0f, -1.0f);
+            s_pb[d * BLOCK + tid] = x[d];
+        }
+        float pbf = fitness<Topo, MODE, TERMS>(cc, x, sh.rest, sh.tgt, nullptr);
+        // swarm argmin + unconditional first global-best copy (src/kernel.cu:297-304)
+        coop_exchange<J, BLOCK>(sh, cs, s_pb, i < P ? ordered_key(pbf) : 0xFFFFFFFFu, io.coop_error, true);
+
+        for (int it = 0; it < io.iterations; ++it) {
+            compiler_fence();
+            if (cs.abort) break;
+            swarm_step<Topo, MODE, TERMS, BLOCK>(cc, sh, s_pb, tid, x, v, pbf, coef, rng);
+            const bool act = cs.member * BLOCK + tid < P;
+            coop_exchange<J, BLOCK>(sh, cs, s_pb, act ? ordered_key(pbf) : 0xFFFFFFFFu, io.coop_error, false);
+        }
+
+        compiler_fence();
+        const int member = cs.member;
+        const int64_t bb = cs.b;
+        const int ii = member * BLOCK + tid;
+        if (member == 0) {  // outputs (updateGlobalBestCoordsKernel) + fitness + residual
+            if (tid < D) io.out_angles[bb * D + tid] = sh.g[tid];
+            if (tid == 0 && io.out_fitness) io.out_fitness[bb] = key_to_float(cs.gkey);
+            if (io.out_residual && tid < 64) {
+                float g[D];
+#pragma unroll
+                for (int d = 0; d < D; ++d) g[d] = sh.g[d];
+                const float r = residual<Topo, MODE>(cc, g, sh.tgt);
+                if (tid == 0) io.out_residual[bb] = r;
+            }
+        }
+        if (ii < P) {
+            store_rng(rng, io.rng + bb * P + ii);
+            if (io.dump_particles) {  // reference particles layout [3][D][P] per swarm
+                float* base = io.dump_particles + bb * (int64_t)3 * D * P;
+#pragma unroll
+                for (int d = 0; d < D; ++d) {
+                    base[(int64_t)d * P + ii] = x[d];
+                    base[(int64_t)(D + d) * P + ii] = v[d];
+                    base[(int64_t)(2 * D + d) * P + ii] = s_pb[d * BLOCK + tid];
+                }
+            }
+            if (io.dump_bests) io.dump_bests[bb * P + ii] = pbf;
+        }
+        __syncthreads();  // sh / s_pb are reused by the next swarm; every wave has read cs
+        if (cs.abort) {     // a wait timed out: mark this and every later swarm of the group as failed
+            for (int64_t r = bb; r < io.num_swarms; r += io.coop_ng)
+                if (member == 0 && tid == 0 && io.out_fitness) io.out_fitness[r] = __builtin_nanf("");
+            break;
+        }
+        if (tid == 0) cs.b = bb + io.coop_ng;
+        __syncthreads();
+    }
+}
+
+// Launch: grid = NG * G workgroups, one per CU, checked for co-residency by
+// hipLaunchCooperativeKernel (an oversized grid is an error, never a hang).
+template <class Topo, int MODE, int TERMS>
+inline hipError_t launch_coop_kernel(const ChainConsts<Topo::J>& cc, const SwarmIO& io, hipStream_t stream)
+{
+    const dim3 grid((unsigned)(io.coop_ng * io.coop_g)), threads(kCoopThreads<Topo::J>());
+    void* args[] = {const_cast<ChainConsts<Topo::J>*>(&cc), const_cast<SwarmIO*>(&io)};
+    return hipLaunchCooperativeKernel(reinterpret_cast<const void*>(&k_swarm_coop<Topo, MODE, TERMS>), grid, threads,
+                                      args, 0, stream);
+}
+
+template <class Topo, int MODE>
+inline hipError_t run_coop(const ChainHost& ch, const SwarmIO& io, hipStream_t stream)
+{
+    const ChainConsts<Topo::J> cc = make_consts<Topo::J>(ch);
+    const int terms = (ch.use_posref ? kTermPosRef : 0) | (ch.use_penalty ? kTermPenalty : 0) |
+                      (ch.uniform_bounds ? kTermUniformBounds : 0) | (ch.num_coll > 0 ? kTermColliders : 0);
+    if constexpr (!Topo::kGeneric && MODE == IKPSO_ARITH_FAST) {
+        if (terms == kTermUniformBounds) return launch_coop_kernel<Topo, MODE, kTermUniformBounds>(cc, io, stream);
+        if (terms == (kTermUniformBounds | kTermPenalty))
+            return launch_coop_kernel<Topo, MODE, kTermUniformBounds | kTermPenalty>(cc, io, stream);
+    }
+    if (ch.num_coll > 0) return launch_coop_kernel<Topo, MODE, kTermRuntime | kTermColliders>(cc, io, stream);
+    return launch_coop_kernel<Topo, MODE, kTermRuntime>(cc, io, stream);
+}
+
+}  // namespace ikpso

@@ -70,6 +70,20 @@ __host__ __device__ constexpr int kResidentMaxThreads()
     return J <= 10 ? 1024 : 256;
 }
 
+// Threads per workgroup of the cooperative kernel: the resident kernel's 1024
+// for short chains; 512 (2 waves per SIMD, <= 256 VGPRs, 120 KiB of local bests
+// at D = 60) for long ones.  One workgroup per CU either way (LDS).
+template <int J>
+__host__ __device__ constexpr int kCoopThreads()
+{
+    return J <= 10 ? 1024 : 512;
+}
+
+// Published record of one chunk: key, global particle index, D floats, padded
+// to a 64-B multiple.
+__host__ __device__ constexpr int kCoopSlot(int D) { return ((D + 2 + 15) / 16) * 16; }
+
+constexpr int kCoopCounterStride = 32;  // one 128-B line per group counter
 template <int J>
 ChainConsts<J> make_consts(const ChainHost& h)
 {
@@ -114,8 +128,16 @@ hipError_t launch_resident(const ChainHost& ch, int mode, const SwarmIO& io, hip
 hipError_t launch_stream(const ChainHost& ch, int mode, const StreamIO& io, int iterations, hipStream_t stream);
 size_t stream_workspace_bytes(int64_t B, int P, int D, bool with_state);
 hipError_t launch_evaluate(const ChainHost& ch, int mode, const EvalIO& io, hipStream_t stream);
+// Cooperative resident kernel (ikpso_coop.h): io.coop_* describe the grid and workspace.
+hipError_t launch_coop(const ChainHost& ch, int mode, const SwarmIO& io, hipStream_t stream);
+// Co-resident workgroups per CU of the cooperative kernel, CU count, threads per workgroup.
+struct CoopGeometry {
+    int threads = 0, blocks_per_cu = 0, cus = 0;
+};
+bool coop_geometry(const ChainHost& ch, int mode, CoopGeometry* g);
+size_t coop_workspace_bytes(int ng, int G, int D);
 int resident_max_threads(const ChainHost& ch);
 bool chain_supported(const ChainHost& ch);
-const char* kernel_name(const ChainHost& ch, bool streaming);
+const char* kernel_name(const ChainHost& ch, int family);  // IKPSO_KERNEL_*
 
 }  // namespace ikpso

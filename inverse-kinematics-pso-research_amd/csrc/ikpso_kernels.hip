@@ -18,6 +18,7 @@
 #include "ikpso_device.h"
 #include "ikpso_kernels.h"
 #include "ikpso_swarm.h"
+#include "ikpso_coop.h"
 #include "ikpso_topo_ops.h"
 
 namespace ikpso {
@@ -68,8 +69,20 @@ bool chain_supported(const ChainHost& ch)
     return visit_topology(ch, [](auto) {});
 }
 
-const char* kernel_name(const ChainHost& ch, bool streaming)
+const char* kernel_name(const ChainHost& ch, int family)
 {
+    const bool streaming = family == IKPSO_KERNEL_STREAMING;
+    if (family == IKPSO_KERNEL_COOP) {
+        const char* name = "swarm_coop<generic>";
+        visit_topology(ch, [&](auto topo) {
+            using T = decltype(topo);
+            if constexpr (std::is_same_v<T, TopoRef7>) name = "swarm_coop<ref_tree7>";
+            else if constexpr (std::is_same_v<T, TopoSerialTip<6>>) name = "swarm_coop<serial_tip6>";
+            else if constexpr (std::is_same_v<T, TopoSerialTip<7>>) name = "swarm_coop<serial_tip7>";
+            else if constexpr (std::is_same_v<T, TopoSerialTip<20>>) name = "swarm_coop<serial_tip20>";
+        });
+        return name;
+    }
     const char* name = streaming ? "swarm_streaming<generic>" : "swarm_resident<generic>";
     visit_topology(ch, [&](auto topo) {
         using T = decltype(topo);
@@ -108,6 +121,48 @@ hipError_t launch_evaluate(const ChainHost& ch, int mode, const EvalIO& io, hipS
         err = TopoOps<T>::evaluate(ch, mode, io, stream);
     });
     return ok ? err : hipErrorInvalidValue;
+}
+
+hipError_t launch_coop(const ChainHost& ch, int mode, const SwarmIO& io, hipStream_t stream)
+{
+    if (io.num_swarms <= 0) return hipSuccess;
+    if (!ch.aux_dev || io.coop_g <= 0 || io.coop_ng <= 0 || io.coop_ng % 8 != 0 || !io.coop_counter ||
+        !io.coop_slots || !io.coop_error)
+        return hipErrorInvalidValue;
+    hipError_t err = hipErrorInvalidValue;
+    const bool ok = visit_topology(ch, [&](auto topo) {
+        using T = decltype(topo);
+        if (io.coop_g * kCoopThreads<T::J>() < io.P || io.coop_g > 64) return;  // G chunks must cover the swarm
+        err = TopoOps<T>::coop(ch, mode, io, stream);
+    });
+    return ok ? err : hipErrorInvalidValue;
+}
+
+// One cooperative workgroup per CU: the kernel's LDS block is at least 82 KiB
+// (more than half of a CU's 160 KiB), whatever the topology.
+bool coop_geometry(const ChainHost& ch, int mode, CoopGeometry* g)
+{
+    (void)mode;
+    bool spec = false;
+    visit_topology(ch, [&](auto topo) {
+        using T = decltype(topo);
+        if constexpr (!T::kGeneric) {
+            g->threads = kCoopThreads<T::J>();
+            spec = true;
+        }
+    });
+    if (!spec) return false;
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0) != hipSuccess || cus <= 0) return false;
+    g->blocks_per_cu = 1;
+    g->cus = cus;
+    return true;
+}
+
+size_t coop_workspace_bytes(int ng, int G, int D)
+{
+    return sizeof(uint32_t) * (size_t)ng * kCoopCounterStride + sizeof(float) * (size_t)ng * 2 * G * kCoopSlot(D) +
+           256 + 3 * 256;
 }
 
 hipError_t launch_stream(const ChainHost& ch, int mode, const StreamIO& io, int iterations, hipStream_t stream)

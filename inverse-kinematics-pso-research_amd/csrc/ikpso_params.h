@@ -50,6 +50,12 @@ struct SwarmIO {
     int32_t P;
     int32_t iterations;
     int64_t num_swarms;
+    // cooperative kernel only (ikpso_coop.h): G workgroups per swarm, NG groups
+    uint32_t* coop_counter;   // [NG][32] arrival counters (zeroed before the launch)
+    float* coop_slots;        // [NG][2][G][kCoopSlot(D)] published chunk minima
+    int32_t* coop_error;      // set to 1 if a group wait timed out
+    int32_t coop_g;
+    int32_t coop_ng;
 };
 
 // Streaming (state-in-HBM) kernels: one launch per PSO iteration over every

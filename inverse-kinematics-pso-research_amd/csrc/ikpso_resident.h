@@ -21,6 +21,74 @@
 
 namespace ikpso {
 
+// One PSO iteration of one particle (lane `tid`) of a swarm whose local bests
+// sit in LDS as s_pb[d * BLOCK + lane] (shared by the resident and cooperative
+// kernels).  simulateParticlesKernel (src/kernel.cu:153-189) + calculateDistance
+// (src/kernel.cu:64-151), one node at a time: the node's three angles
+// are updated (r1, r2, r3 per dimension, in dimension order) and
+// clamped, then the node is folded into the FK/fitness.  A node's FK
+// needs only its own and its ancestors' angles, so this computes the
+// reference's update-all-then-evaluate values in the same order.  The
+// node's LDS operands (local best, global best, rest pose, target) are
+// loaded one node ahead so their latency hides under the previous node.
+template <class Topo, int MODE, int TERMS, int BLOCK>
+__device__ __forceinline__ void swarm_step(const ChainConsts<Topo::J>& cc, SwarmShared<Topo::J>& sh, float* s_pb,
+                                           int tid, float (&x)[3 * Topo::J], float (&v)[3 * Topo::J], float& pbf,
+                                           const PsoCoef& coef, Xorwow& rng)
+{
+    constexpr int J = Topo::J;
+    constexpr int D = 3 * J;
+    FitnessAcc<Topo, MODE, TERMS> acc(cc);
+    float npb[3], ng[3], nrest[3], ntgt[3];
+#pragma unroll
+    for (int ax = 0; ax < 3; ++ax) {
+        npb[ax] = s_pb[ax * BLOCK + tid];
+        ng[ax] = sh.g[ax];
+        nrest[ax] = sh.rest[ax];
+        ntgt[ax] = Topo::effector(1) ? sh.tgt[ax] : 0.0f;
+    }
+#pragma unroll
+    for (int k = 1; k <= J; ++k) {
+        float cpb[3], cg[3], crest[3], ctgt[3];
+#pragma unroll
+        for (int ax = 0; ax < 3; ++ax) {
+            cpb[ax] = npb[ax];
+            cg[ax] = ng[ax];
+            crest[ax] = nrest[ax];
+            ctgt[ax] = ntgt[ax];
+        }
+        if (k < J) {
+#pragma unroll
+            for (int ax = 0; ax < 3; ++ax) {
+                const int d = 3 * k + ax;
+                npb[ax] = s_pb[d * BLOCK + tid];
+                ng[ax] = sh.g[d];
+                nrest[ax] = sh.rest[d];
+                ntgt[ax] = Topo::effector(k + 1) ? sh.tgt[d] : 0.0f;
+            }
+        }
+#pragma unroll
+        for (int ax = 0; ax < 3; ++ax) {
+            const int d = 3 * (k - 1) + ax;
+            pso_update<MODE>(x[d], v[d], cpb[ax], cg[ax], coef, rng);
+            if constexpr (TERMS & kTermUniformBounds)
+                x[d] = clamp_ref(x[d], cc.lo[0], cc.hi[0]);
+            else
+                x[d] = clamp_ref(x[d], sh.lo[d], sh.hi[d]);
+        }
+        acc.node(cc, k, x[3 * (k - 1)], x[3 * (k - 1) + 1], x[3 * (k - 1) + 2], crest, ctgt, nullptr);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+
+    // updateLocalBests (src/kernel.cu:202-221): strict improvement
+    const float f = acc.finish(cc);
+    if (f < pbf) {
+        pbf = f;
+#pragma unroll
+        for (int d = 0; d < D; ++d) s_pb[d * BLOCK + tid] = x[d];
+    }
+}
+
 // ------------------------------------------------------- resident swarm kernel
 template <class Topo, int MODE, int TERMS>
 __global__ void __launch_bounds__(kResidentMaxThreads<Topo::J>())
@@ -65,63 +133,7 @@ __global__ void __launch_bounds__(kResidentMaxThreads<Topo::J>())
     const PsoCoef coef = pso_coef(cc);
     for (int it = 0; it < io.iterations; ++it) {
         compiler_fence();
-        // simulateParticlesKernel (src/kernel.cu:153-189) + calculateDistance
-        // (src/kernel.cu:64-151), one node at a time: the node's three angles
-        // are updated (r1, r2, r3 per dimension, in dimension order) and
-        // clamped, then the node is folded into the FK/fitness.  A node's FK
-        // needs only its own and its ancestors' angles, so this computes the
-        // reference's update-all-then-evaluate values in the same order.  The
-        // node's LDS operands (local best, global best, rest pose, target) are
-        // loaded one node ahead so their latency hides under the previous node.
-        FitnessAcc<Topo, MODE, TERMS> acc(cc);
-        float npb[3], ng[3], nrest[3], ntgt[3];
-#pragma unroll
-        for (int ax = 0; ax < 3; ++ax) {
-            npb[ax] = s_pb[ax * BLOCK + tid];
-            ng[ax] = sh.g[ax];
-            nrest[ax] = sh.rest[ax];
-            ntgt[ax] = Topo::effector(1) ? sh.tgt[ax] : 0.0f;
-        }
-#pragma unroll
-        for (int k = 1; k <= J; ++k) {
-            float cpb[3], cg[3], crest[3], ctgt[3];
-#pragma unroll
-            for (int ax = 0; ax < 3; ++ax) {
-                cpb[ax] = npb[ax];
-                cg[ax] = ng[ax];
-                crest[ax] = nrest[ax];
-                ctgt[ax] = ntgt[ax];
-            }
-            if (k < J) {
-#pragma unroll
-                for (int ax = 0; ax < 3; ++ax) {
-                    const int d = 3 * k + ax;
-                    npb[ax] = s_pb[d * BLOCK + tid];
-                    ng[ax] = sh.g[d];
-                    nrest[ax] = sh.rest[d];
-                    ntgt[ax] = Topo::effector(k + 1) ? sh.tgt[d] : 0.0f;
-                }
-            }
-#pragma unroll
-            for (int ax = 0; ax < 3; ++ax) {
-                const int d = 3 * (k - 1) + ax;
-                pso_update<MODE>(x[d], v[d], cpb[ax], cg[ax], coef, rng);
-                if constexpr (TERMS & kTermUniformBounds)
-                    x[d] = clamp_ref(x[d], cc.lo[0], cc.hi[0]);
-                else
-                    x[d] = clamp_ref(x[d], sh.lo[d], sh.hi[d]);
-            }
-            acc.node(cc, k, x[3 * (k - 1)], x[3 * (k - 1) + 1], x[3 * (k - 1) + 2], crest, ctgt, nullptr);
-            __builtin_amdgcn_sched_barrier(0);
-        }
-
-        // updateLocalBests (src/kernel.cu:202-221): strict improvement
-        const float f = acc.finish(cc);
-        if (f < pbf) {
-            pbf = f;
-#pragma unroll
-            for (int d = 0; d < D; ++d) s_pb[d * BLOCK + tid] = x[d];
-        }
+        swarm_step<Topo, MODE, TERMS, BLOCK>(cc, sh, s_pb, tid, x, v, pbf, coef, rng);
 
         // thrust::min_element + `globalMin > currentGlobalMin` (src/kernel.cu:315-323)
 #if IKPSO_ABL_NOSYNC  // timing-only ablation: no swarm argmin

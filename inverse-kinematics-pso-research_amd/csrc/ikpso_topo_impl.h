@@ -2,6 +2,7 @@
 // ikpso_inst_*.hip translation units, followed by explicit instantiations.
 #pragma once
 
+#include "ikpso_coop.h"
 #include "ikpso_resident.h"
 #include "ikpso_stream.h"
 #include "ikpso_topo_ops.h"
@@ -24,6 +25,15 @@ template <class Topo, int MODE>
 hipError_t ModeOps<Topo, MODE>::evaluate(const ChainHost& ch, const EvalIO& io, hipStream_t s)
 {
     return run_evaluate<Topo, MODE>(ch, io, s);
+}
+
+template <class Topo, int MODE>
+hipError_t ModeOps<Topo, MODE>::coop(const ChainHost& ch, const SwarmIO& io, hipStream_t s)
+{
+    if constexpr (Topo::kGeneric)
+        return hipErrorNotSupported;  // generic trees take the streaming kernels
+    else
+        return run_coop<Topo, MODE>(ch, io, s);
 }
 
 }  // namespace ikpso

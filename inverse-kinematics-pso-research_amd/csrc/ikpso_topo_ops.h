@@ -15,6 +15,7 @@ struct ModeOps {
     static hipError_t resident(const ChainHost& ch, const SwarmIO& io, int block, hipStream_t stream);
     static hipError_t stream(const ChainHost& ch, const StreamIO& io, int iterations, hipStream_t stream);
     static hipError_t evaluate(const ChainHost& ch, const EvalIO& io, hipStream_t stream);
+    static hipError_t coop(const ChainHost& ch, const SwarmIO& io, hipStream_t stream);
 };
 
 template <class Topo>
@@ -33,6 +34,11 @@ struct TopoOps {
     {
         return mode == IKPSO_ARITH_REFERENCE ? ModeOps<Topo, IKPSO_ARITH_REFERENCE>::evaluate(ch, io, s)
                                              : ModeOps<Topo, IKPSO_ARITH_FAST>::evaluate(ch, io, s);
+    }
+    static hipError_t coop(const ChainHost& ch, int mode, const SwarmIO& io, hipStream_t s)
+    {
+        return mode == IKPSO_ARITH_REFERENCE ? ModeOps<Topo, IKPSO_ARITH_REFERENCE>::coop(ch, io, s)
+                                             : ModeOps<Topo, IKPSO_ARITH_FAST>::coop(ch, io, s);
     }
 };
 

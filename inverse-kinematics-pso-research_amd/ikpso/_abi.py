@@ -31,6 +31,7 @@ ARITH_REFERENCE = 1
 KERNEL_AUTO = 0
 KERNEL_RESIDENT = 1
 KERNEL_STREAMING = 2
+KERNEL_COOP = 3
 
 # ------------------------------------------------------------ numpy layouts
 #: NodeCUDA (src/Particle.h:24-39), 88 bytes.

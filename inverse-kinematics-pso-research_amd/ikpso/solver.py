@@ -188,7 +188,7 @@ class BatchSolver:
         desc.fit = fit.c()
         desc.arith = {"fast": _abi.ARITH_FAST, "reference": _abi.ARITH_REFERENCE}[arith]
         desc.kernel = {"auto": _abi.KERNEL_AUTO, "resident": _abi.KERNEL_RESIDENT,
-                       "streaming": _abi.KERNEL_STREAMING}[kernel]
+                       "streaming": _abi.KERNEL_STREAMING, "coop": _abi.KERNEL_COOP}[kernel]
         desc.positions = _any_ptr(None if positions is None else np.asarray(positions, np.float32), keep)
         desc.limit_weight = float(limit_weight)
         desc.soft_lo = _any_ptr(None if soft_lo is None else np.asarray(soft_lo, np.float32), keep)

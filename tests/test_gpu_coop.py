@@ -1,0 +1,81 @@
+"""Cooperative resident kernel (csrc/ikpso_coop.h): one swarm over G
+co-resident workgroups exchanging chunk minima through L2 every iteration.
+Same algorithm and draw order as the reference, so REFERENCE arithmetic is
+compared with the oracle bit for bit, including swarms that are not a
+multiple of the workgroup size and groups that solve several swarms in turn."""
+import numpy as np
+import pytest
+
+import ikpso
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+def dev(x):
+    return torch.from_numpy(np.ascontiguousarray(x)).cuda()
+
+
+@pytest.mark.parametrize("P,I", [(2048, 20), (3000, 7)])
+def test_coop_compat_reference_bitexact(oracle, device, monkeypatch, P, I):
+    chain = ikpso.reference_scene(reset=True).origin.to_cuda()
+    monkeypatch.setenv("IKPSO_ARITH", "reference")
+    monkeypatch.setenv("IKPSO_KERNEL", "coop")
+    D = 21
+    parts = ikpso.particles_tensor(P, D)
+    bests = torch.zeros(P, dtype=torch.float32, device="cuda")
+    r = ikpso.rng_tensor(P)
+    assert ikpso.init_generators(r, P) == 0
+    res = np.zeros(D, dtype=np.float32)
+    assert ikpso.calculate_pso(parts, None, bests, r, P, chain, ikpso.PSOConfig(0.5, 0.5, 1.25, I),
+                               ikpso.MAIN_FITNESS, res) == 0
+    ostate = oracle.init_generators(P, 0)
+    ores, oparts, obests = oracle.calculate_pso(chain, P, ostate, iterations=I)
+    assert np.array_equal(r.cpu().numpy()[:, :6], ostate.view(np.int32).reshape(P, 12)[:, :6])
+    assert np.array_equal(bests.cpu().numpy(), obests)
+    assert np.array_equal(parts.cpu().numpy(), oparts)
+    assert np.array_equal(res, ores)
+
+
+def test_coop_batch_groups_loop_over_swarms(oracle, device):
+    """P = 16384 (G = 16 workgroups per swarm, at most 16 concurrent groups on 256
+    CUs): 20 swarms, so some groups solve two swarms back to back."""
+    wl = ikpso.workload(3)
+    B, P, I = 20, 16384, 4
+    tg = wl.targets(0, B)
+    s = ikpso.BatchSolver(wl.chain, P, pso=ikpso.PSOConfig(0.5, 0.5, 1.25, I), arith="reference", kernel="coop")
+    assert "coop" in s.kernel
+    s.seed(B)
+    ang, fit, res = (t.cpu().numpy() for t in s.solve(dev(tg), iterations=I))
+    s.close()
+    ostate = oracle.init_generators(B * P, 0)
+    oang, ofit, ores = oracle.solve_batch(wl.chain, tg, None, P, I, ostate, threads=8)
+    assert np.array_equal(ang, oang) and np.array_equal(fit, ofit)
+    assert np.max(np.abs(res - ores)) < 1e-5
+
+
+def test_coop_equals_streaming(device):
+    """FAST: the two multi-workgroup families agree to the FAST tolerance; their
+    generator streams (integer work) are identical."""
+    wl = ikpso.workload(3)
+    B, P, I = 16, 4096, 30
+    tg = wl.targets(0, B)
+    out = []
+    for kern in ("coop", "streaming"):
+        s = ikpso.BatchSolver(wl.chain, P, pso=ikpso.PSOConfig(0.5, 0.5, 1.25, I), kernel=kern)
+        s.seed(B)
+        out.append([t.cpu().numpy() for t in s.solve(dev(tg), iterations=I)])
+        s.close()
+    (a1, f1, r1), (a2, f2, r2) = out
+    assert np.all(np.isfinite(f1))
+    assert np.mean(np.abs(f1 - f2) / f2 <= 1e-3) >= 0.75
+    assert abs(f1.mean() - f2.mean()) / f2.mean() < 5e-3
+
+
+def test_coop_visualiser_swarm_auto(oracle, device, monkeypatch):
+    """AUTO picks the cooperative kernel for the visualiser's N = 16384."""
+    chain = ikpso.reference_scene(reset=True).origin.to_cuda()
+    s = ikpso.BatchSolver(chain, 16384)
+    assert "coop" in s.kernel
+    s.close()

@@ -287,11 +287,14 @@ def test_empty_and_invalid(device, scene_chain):
 
 
 # ------------------------------------------------------ streaming kernels
+@pytest.mark.parametrize("kernel", ["streaming", "coop"])
 @pytest.mark.parametrize("arith", ["fast", "reference"])
 @pytest.mark.parametrize("P,I", [(2048, 0), (2048, 1), (1500, 20)])
-def test_streaming_compat_vs_oracle(oracle, device, scene_chain, monkeypatch, arith, P, I):
-    """P > 1024 takes the streaming kernels automatically (state in the caller's particles buffer)."""
+def test_streaming_compat_vs_oracle(oracle, device, scene_chain, monkeypatch, arith, P, I, kernel):
+    """P > 1024: the streaming kernels (state in the caller's particles buffer)
+    and the cooperative kernel (the swarm over G = 2 workgroups) -- AUTO picks coop."""
     monkeypatch.setenv("IKPSO_ARITH", arith)
+    monkeypatch.setenv("IKPSO_KERNEL", kernel)
     res, parts, bests, r = run_compat(scene_chain, P, I, arith)
     ostate = oracle.init_generators(P, 0)
     ores, oparts, obests = oracle.calculate_pso(scene_chain, P, ostate, iterations=I)
@@ -345,16 +348,18 @@ def test_batch_streaming_equals_resident(device, batch_case):
         assert np.array_equal(x, y)
 
 
+@pytest.mark.parametrize("kernel", ["streaming", "coop"])
 @pytest.mark.parametrize("arith", ["fast", "reference"])
-def test_config5_chain_with_penalty(oracle, device, arith):
+def test_config5_chain_with_penalty(oracle, device, arith, kernel):
     """BASELINE config 5 shape at test size: 20-joint serial chain (D = 60), tip
-    effector, soft joint-limit penalty (extension), streaming kernels."""
+    effector, soft joint-limit penalty (extension); streaming and cooperative
+    kernels (P = 1024: two 512-lane chunks per swarm)."""
     wl = ikpso.workload(5)
-    B, P, I = 3, 512, 10
+    B, P, I = 3, 1024, 10
     tg = wl.targets(0, B)
     s = ikpso.BatchSolver(wl.chain, P, pso=ikpso.PSOConfig(0.5, 0.5, 1.25, I), arith=arith,
-                          limit_weight=wl.limit_weight, soft_lo=wl.soft_lo, soft_hi=wl.soft_hi)
-    assert "streaming" in s.kernel and "serial_tip20" in s.kernel
+                          limit_weight=wl.limit_weight, soft_lo=wl.soft_lo, soft_hi=wl.soft_hi, kernel=kernel)
+    assert kernel in s.kernel and "serial_tip20" in s.kernel
     s.seed(B)
     ang, fit, res = (t.cpu().numpy() for t in s.solve(dev(tg), iterations=I))
     ostate = oracle.init_generators(B * P, 0)
