@@ -44,21 +44,25 @@ def parse():
     ap.add_argument("--particles", type=int, default=None)
     ap.add_argument("--iterations", type=int, default=None)
     ap.add_argument("--arith", choices=["fast", "reference"], default="fast")
+    ap.add_argument("--kernel", choices=["auto", "resident", "coop", "streaming"], default="auto",
+                    help="kernel family (auto: resident if the swarm fits one workgroup, else cooperative)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU baseline sample (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     return ap.parse_args()
 
 
-def valu_per_update():
-    """VALU lane-instructions per particle-update of the resident kernel, from
-    the committed rocprofv3 SQ_INSTS_VALU measurement (profiles/), else None."""
+def valu_per_update(kernel: str):
+    """VALU lane-instructions per particle-update of `kernel` (the solver's
+    kernel name), from the committed rocprofv3 SQ_INSTS_VALU measurement
+    (profiles/valu_per_update.json, tools/update_profiles.py), else None."""
     f = ROOT / "profiles" / "valu_per_update.json"
-    if f.exists():
-        try:
-            return json.loads(f.read_text())
-        except Exception:
-            return None
-    return None
+    if not f.exists():
+        return None
+    try:
+        db = json.loads(f.read_text())
+    except Exception:
+        return None
+    return db.get(kernel)
 
 
 def cpu_baseline(wl, seconds: float, threads: int):
@@ -121,7 +125,8 @@ def main():
     first = rank * Bl
     targets = torch.from_numpy(wl.targets(first, Bl)).to(dev)
     solver = ikpso.BatchSolver(wl.chain, P, pso=ikpso.PSOConfig(0.5, 0.5, 1.25, I), arith=args.arith,
-                               limit_weight=wl.limit_weight, soft_lo=wl.soft_lo, soft_hi=wl.soft_hi)
+                               limit_weight=wl.limit_weight, soft_lo=wl.soft_lo, soft_hi=wl.soft_hi,
+                               kernel=args.kernel)
     solver.seed(Bl, seed_base=0, first_swarm=first)
     D = solver.dof
     out = (torch.empty((Bl, D), device=dev), torch.empty((Bl,), device=dev), torch.empty((Bl,), device=dev))
@@ -189,7 +194,7 @@ def main():
         alg_bytes = 20 * D + 8
         alg_gbs = ups_launch * alg_bytes / kern_s / 1e9
         streaming = "streaming" in solver.kernel
-        vpu = None if streaming else valu_per_update()
+        vpu = None if streaming else valu_per_update(solver.kernel)
         valu = None
         if vpu:
             ach = ups_launch * vpu["valu_lane_instr_per_update"] / kern_s / 1e12

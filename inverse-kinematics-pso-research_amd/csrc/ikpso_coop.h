@@ -27,7 +27,7 @@
 // time every chunk has read parity p.  Workgroup b sits on XCD b % 8; the G
 // chunks of a group share an XCD (speed only, never correctness).  Waits are
 // bounded: a timed-out wait sets io.coop_error and the kernel drains.
-// Residency is checked at launch (hipLaunchCooperativeKernel).
+// Residency is checked at launch against the occupancy query.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -231,15 +231,24 @@ __global__ void __launch_bounds__(kCoopThreads<Topo::J>(), kCoopThreads<Topo::J>
     }
 }
 
-// Launch: grid = NG * G workgroups, one per CU, checked for co-residency by
-// hipLaunchCooperativeKernel (an oversized grid is an error, never a hang).
+// Launch: grid = NG * G workgroups, at most one per CU.  Co-residency is
+// checked here against the occupancy query (the check hipLaunchCooperativeKernel
+// would make; a plain launch gives the same residency without the cooperative
+// queue): an oversized grid is an error, never a hang.
 template <class Topo, int MODE, int TERMS>
 inline hipError_t launch_coop_kernel(const ChainConsts<Topo::J>& cc, const SwarmIO& io, hipStream_t stream)
 {
-    const dim3 grid((unsigned)(io.coop_ng * io.coop_g)), threads(kCoopThreads<Topo::J>());
-    void* args[] = {const_cast<ChainConsts<Topo::J>*>(&cc), const_cast<SwarmIO*>(&io)};
-    return hipLaunchCooperativeKernel(reinterpret_cast<const void*>(&k_swarm_coop<Topo, MODE, TERMS>), grid, threads,
-                                      args, 0, stream);
+    constexpr int T = kCoopThreads<Topo::J>();
+    const auto kernel = &k_swarm_coop<Topo, MODE, TERMS>;
+    int dev = 0, cus = 0, per_cu = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, T, 0);
+    if (e != hipSuccess) return e;
+    const int64_t grid = (int64_t)io.coop_ng * io.coop_g;
+    if (per_cu < 1 || grid > (int64_t)cus) return hipErrorCooperativeLaunchTooLarge;
+    hipLaunchKernelGGL(kernel, dim3((unsigned)grid), dim3(T), 0, stream, cc, io);
+    return hipGetLastError();
 }
 
 template <class Topo, int MODE>

@@ -1,16 +1,18 @@
 #!/bin/bash
 # rocprofv3 kernel trace + PMC passes (one counter group per pass; no tracing
-# domains combined with --pmc) for the bench workload.  Outputs in gpurun_out/prof_*.
+# domains combined with --pmc) for a bench workload.  Outputs in
+# gpurun_out/<PROF_NAME>_{trace,valu,fetch,write,cycles}.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 ARGS=${PROF_ARGS:-"--swarms-per-gpu 2048 --steps 2 --warmup 1 --cpu-seconds 0"}
-run() {  # run NAME ROCPROF_ARGS...
-  local name=$1; shift
-  echo "== $name"
-  timeout -k 10 600 rocprofv3 "$@" -d "gpurun_out/prof_$name" -o run --output-format csv -- python3 bench.py $ARGS \
-    > "gpurun_out/prof_$name.log" 2>&1
-  local rc=$?; echo "   rc=$rc"; [ $rc -eq 0 ] || { tail -20 "gpurun_out/prof_$name.log"; exit $rc; }
+NAME=${PROF_NAME:-prof}
+run() {  # run PASS ROCPROF_ARGS...
+  local pass=$1; shift
+  echo "== $NAME $pass"
+  timeout -k 10 600 rocprofv3 "$@" -d "gpurun_out/${NAME}_$pass" -o run --output-format csv -- python3 bench.py $ARGS \
+    > "gpurun_out/${NAME}_$pass.log" 2>&1
+  local rc=$?; echo "   rc=$rc"; [ $rc -eq 0 ] || { tail -20 "gpurun_out/${NAME}_$pass.log"; exit $rc; }
 }
 run trace --kernel-trace --stats
 run valu --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVES GRBM_GUI_ACTIVE
