@@ -16,6 +16,12 @@
 #include "ikpso_collide.h"
 #include "ikpso_params.h"
 
+#ifndef IKPSO_SINCOS_V2
+#define IKPSO_SINCOS_V2 1
+#endif
+#ifndef IKPSO_CLAMP_MED3
+#define IKPSO_CLAMP_MED3 1
+#endif
 #ifndef IKPSO_SCHED_NODE
 #define IKPSO_SCHED_NODE 0
 #endif
@@ -134,8 +140,18 @@ __host__ __device__ __forceinline__ void sincos_fast(float x, float* s_out, floa
     *c_out = __builtin_fmaf(-0.5f, x, 1.0f);
     return;
 #endif
+#if IKPSO_SINCOS_V2
+    // Quadrant by the round-to-integer magic constant: k_big = x*2/pi + 1.5*2^23
+    // holds q = rint(x*2/pi) in its low mantissa bits (one FMA instead of a
+    // multiply, a rint and a float->int conversion); the swap of sin and cos
+    // by a bitfield-extended mask and two bitop3 selects.
+    const float kb = __builtin_fmaf(x, 0.636619772367581343f, 12582912.0f);
+    const float k = kb - 12582912.0f;
+    const uint32_t qb = as_uint(kb);
+#else
     const float k = __builtin_rintf(x * 0.636619772367581343f);
     const int q = (int)k;
+#endif
     float r = __builtin_fmaf(-k, 1.57079637050628662109375f, x);
     r = __builtin_fmaf(-k, -4.37113900018624283e-8f, r);
     const float z = r * r;
@@ -145,10 +161,25 @@ __host__ __device__ __forceinline__ void sincos_fast(float x, float* s_out, floa
                               4.166664568298827e-2f);
     cp = __builtin_fmaf(cp, z, -0.5f);
     const float cv = __builtin_fmaf(cp, z, 1.0f);
+#if IKPSO_SINCOS_V2
+#if defined(__HIP_DEVICE_COMPILE__)
+    const uint32_t m = (uint32_t)__builtin_amdgcn_sbfe((int)qb, 0, 1);  // q odd: all ones
+    const uint32_t s1 = __builtin_amdgcn_bitop3_b32(m, as_uint(cv), as_uint(sv), 0xCA);  // m ? cv : sv
+    const uint32_t c1 = __builtin_amdgcn_bitop3_b32(m, as_uint(sv), as_uint(cv), 0xCA);  // m ? sv : cv
+#else
+    const uint32_t m = (qb & 1u) ? 0xFFFFFFFFu : 0u;
+    const uint32_t s1 = (m & as_uint(cv)) | (~m & as_uint(sv));
+    const uint32_t c1 = (m & as_uint(sv)) | (~m & as_uint(cv));
+#endif
+    const uint32_t t = qb << 30;  // bit 31: q & 2 (sin sign); (q + 1) & 2 for cos
+    *s_out = as_float(xor_sign(s1, t));
+    *c_out = as_float(xor_sign(c1, t + 0x40000000u));
+#else
     const bool swap = q & 1;
     const uint32_t t = (uint32_t)q << 30;  // bit 31: q & 2 (sin sign); (q + 1) & 2 for cos
     *s_out = as_float(xor_sign(as_uint(swap ? cv : sv), t));
     *c_out = as_float(xor_sign(as_uint(swap ? sv : cv), t + 0x40000000u));
+#endif
 }
 
 // REFERENCE: the reduction and the polynomials (fdlibm __kernel_sin /
@@ -502,6 +533,17 @@ __device__ __forceinline__ void pso_update(float& x, float& v, float pb, float g
 
 // clamp (src/matrix_operations.cuh:187-190)
 __device__ __forceinline__ float clamp_ref(float v, float lo, float hi) { return fminf(fmaxf(v, lo), hi); }
+
+// FAST mode: one v_med3_f32 (the median of v, lo, hi is the clamp for lo <= hi
+// and finite v); REFERENCE mode keeps the reference's fmaxf/fminf pair.
+template <int MODE>
+__device__ __forceinline__ float clamp_mode(float v, float lo, float hi)
+{
+#if IKPSO_CLAMP_MED3
+    if constexpr (MODE == IKPSO_ARITH_FAST) return __builtin_amdgcn_fmed3f(v, lo, hi);
+#endif
+    return clamp_ref(v, lo, hi);
+}
 
 // ------------------------------------------------------------- reductions
 // Order-preserving map of an fp32 value to uint32 (-0 canonicalised to +0) so

@@ -72,12 +72,14 @@ __device__ __forceinline__ void swarm_step(const ChainConsts<Topo::J>& cc, Swarm
             const int d = 3 * (k - 1) + ax;
             pso_update<MODE>(x[d], v[d], cpb[ax], cg[ax], coef, rng);
             if constexpr (TERMS & kTermUniformBounds)
-                x[d] = clamp_ref(x[d], cc.lo[0], cc.hi[0]);
+                x[d] = clamp_mode<MODE>(x[d], cc.lo[0], cc.hi[0]);
             else
-                x[d] = clamp_ref(x[d], sh.lo[d], sh.hi[d]);
+                x[d] = clamp_mode<MODE>(x[d], sh.lo[d], sh.hi[d]);
         }
         acc.node(cc, k, x[3 * (k - 1)], x[3 * (k - 1) + 1], x[3 * (k - 1) + 2], crest, ctgt, nullptr);
+#if !IKPSO_RES_NO_NODE_BARRIER
         __builtin_amdgcn_sched_barrier(0);
+#endif
     }
 
     // updateLocalBests (src/kernel.cu:202-221): strict improvement

@@ -206,9 +206,9 @@ __global__ void __launch_bounds__(kStreamChunk) k_stream_step(const ChainConsts<
                 pso_update<MODE>(cx[ax], cv[ax], cpb[ax], sh.g[d], coef, rng);
                 pl.st(1, d, cv[ax]);
                 if constexpr (TERMS & kTermUniformBounds)
-                    cx[ax] = clamp_ref(cx[ax], cc.lo[0], cc.hi[0]);
+                    cx[ax] = clamp_mode<MODE>(cx[ax], cc.lo[0], cc.hi[0]);
                 else
-                    cx[ax] = clamp_ref(cx[ax], sh.lo[d], sh.hi[d]);
+                    cx[ax] = clamp_mode<MODE>(cx[ax], sh.lo[d], sh.hi[d]);
                 pl.st(0, d, cx[ax]);
             }
             acc.node(cc, kn, cx[0], cx[1], cx[2], sh.rest + 3 * (kn - 1), sh.tgt + 3 * (kn - 1), nullptr);
