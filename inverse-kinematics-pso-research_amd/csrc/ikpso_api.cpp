@@ -304,26 +304,43 @@ int env_kernel()
     return IKPSO_KERNEL_AUTO;
 }
 
-// Cooperative launch plan for swarms of P particles: G workgroups per swarm,
-// NG concurrent groups (a multiple of 8 for the XCD-aware membership, at most
-// one workgroup per CU, at most ceil8(B) groups).  False if infeasible.
-bool coop_plan(const ChainHost& ch, int mode, int P, int64_t B, int* G, int* NG)
+// Cooperative launch plan for B swarms of P particles: chunk size (the
+// throughput block, or with `latency` the 256-lane block when every swarm then
+// still gets its own CUs), G chunks per swarm, NG concurrent groups (a
+// multiple of 8 for the XCD-aware membership, one workgroup per CU, at most
+// ceil8(B)).  False if infeasible.
+bool coop_plan(const ChainHost& ch, int mode, int P, int64_t B, bool latency, int* G, int* NG, int* block)
 {
     CoopGeometry geo;
     if (!coop_geometry(ch, mode, &geo)) return false;
-    const int g = (P + geo.threads - 1) / geo.threads;
+    int T = geo.threads;
+    if (latency && geo.latency_variant) {
+        const int gl = (P + kCoopLatencyThreads - 1) / kCoopLatencyThreads;
+        if (gl <= 64 && B * gl <= (int64_t)geo.cus && ((geo.cus / gl) & ~7) >= 8) T = kCoopLatencyThreads;
+    }
+    const int g = (P + T - 1) / T;
     int ng = (geo.cus * geo.blocks_per_cu / g) & ~7;
     if (g > 64 || ng < 8) return false;
     const int64_t want = ((B + 7) / 8) * 8;
     if (want < ng) ng = (int)want;
     *G = g;
     *NG = ng;
+    *block = T;
     return true;
+}
+
+// AUTO for a swarm that fits one workgroup: the latency variant of the
+// cooperative kernel when every swarm gets its own CUs (a few swarms: more
+// CUs per swarm), else the resident kernel.
+bool prefer_latency_coop(const ChainHost& ch, int mode, int P, int64_t B)
+{
+    int G, NG, T;
+    return coop_plan(ch, mode, P, B, true, &G, &NG, &T) && T == kCoopLatencyThreads;
 }
 
 // Point the coop fields of `io` into workspace `ws` (coop_workspace_bytes) and
 // clear the counters and the error flag.
-hipError_t carve_coop(SwarmIO& io, void* ws, int G, int NG, int D, hipStream_t s)
+hipError_t carve_coop(SwarmIO& io, void* ws, int G, int NG, int block, int D, hipStream_t s)
 {
     Carver cv{static_cast<char*>(ws)};
     io.coop_counter = cv.take<uint32_t>((size_t)NG * kCoopCounterStride);
@@ -331,6 +348,7 @@ hipError_t carve_coop(SwarmIO& io, void* ws, int G, int NG, int D, hipStream_t s
     io.coop_slots = cv.take<float>((size_t)NG * 2 * G * kCoopSlot(D));
     io.coop_g = G;
     io.coop_ng = NG;
+    io.coop_block = block;
     const size_t zero = reinterpret_cast<char*>(io.coop_slots) - static_cast<char*>(ws);
     return hipMemsetAsync(ws, 0, zero, s);
 }
@@ -339,8 +357,8 @@ hipError_t carve_coop(SwarmIO& io, void* ws, int G, int NG, int D, hipStream_t s
 int pick_kernel(const ChainHost& ch, int mode, int P, int requested)
 {
     const bool fits = P <= resident_max_threads(ch);
-    int G, NG;
-    const bool coop = coop_plan(ch, mode, P, 1, &G, &NG);
+    int G, NG, T;
+    const bool coop = coop_plan(ch, mode, P, 1, false, &G, &NG, &T);
     if (requested == IKPSO_KERNEL_RESIDENT) return fits ? IKPSO_KERNEL_RESIDENT : -1;
     if (requested == IKPSO_KERNEL_STREAMING) return IKPSO_KERNEL_STREAMING;
     if (requested == IKPSO_KERNEL_COOP) return coop ? IKPSO_KERNEL_COOP : -1;
@@ -353,7 +371,8 @@ struct ikpso_solver {
     ChainHost chain;
     float* aux = nullptr;  // device copy of chain.aux
     int family = IKPSO_KERNEL_RESIDENT;
-    void* ws = nullptr;    // streaming workspace
+    int requested = IKPSO_KERNEL_AUTO;
+    void* ws = nullptr;    // streaming / cooperative workspace
     size_t ws_bytes = 0;
     int P = 0;
     int mode = IKPSO_ARITH_FAST;
@@ -435,8 +454,13 @@ ikpso_status ikpso_calculate_pso(float* particles, const float* positions, float
     const int mode = (env && strcmp(env, "reference") == 0) ? IKPSO_ARITH_REFERENCE : IKPSO_ARITH_FAST;
     const int family = pick_kernel(ch, mode, size, env_kernel());
     if (family < 0) return IKPSO_ERR_UNSUPPORTED;
-    int cg = 0, cng = 0;
-    if (family == IKPSO_KERNEL_COOP && !coop_plan(ch, mode, size, 1, &cg, &cng)) return IKPSO_ERR_UNSUPPORTED;
+    int family_run = family;
+    if (family == IKPSO_KERNEL_RESIDENT && env_kernel() == IKPSO_KERNEL_AUTO && prefer_latency_coop(ch, mode, size, 1))
+        family_run = IKPSO_KERNEL_COOP;
+    int cg = 0, cng = 0, cblk = 0;
+    if (family_run == IKPSO_KERNEL_COOP &&
+        !coop_plan(ch, mode, size, 1, env_kernel() == IKPSO_KERNEL_AUTO, &cg, &cng, &cblk))
+        return IKPSO_ERR_UNSUPPORTED;
 
     std::lock_guard<std::mutex> lk(g_scratch_mu);
     // device scratch: [result D | aux (64-float aligned) | streaming workspace];
@@ -444,16 +468,16 @@ ikpso_status ikpso_calculate_pso(float* particles, const float* positions, float
     // `ch.aux` outlives every use
     const size_t aux_at = ((size_t)D + 63) & ~size_t(63);
     const size_t head = sizeof(float) * (aux_at + ch.aux.size());
-    const size_t ws = family == IKPSO_KERNEL_STREAMING ? stream_workspace_bytes(1, size, D, false)
-                      : family == IKPSO_KERNEL_COOP    ? coop_workspace_bytes(cng, cg, D)
-                                                       : 0;
+    const size_t ws = family_run == IKPSO_KERNEL_STREAMING ? stream_workspace_bytes(1, size, D, false)
+                      : family_run == IKPSO_KERNEL_COOP    ? coop_workspace_bytes(cng, cg, D)
+                                                           : 0;
     float* dres = nullptr;
     st = scratch(((head + 255) & ~size_t(255)) + ws, &dres);
     if (st != IKPSO_OK) return st;
     const hipStream_t s = (hipStream_t)stream;
     IKPSO_HIP(hipMemcpyAsync(dres + aux_at, ch.aux.data(), sizeof(float) * ch.aux.size(), hipMemcpyHostToDevice, s));
     ch.aux_dev = dres + aux_at;
-    if (family == IKPSO_KERNEL_RESIDENT) {
+    if (family_run == IKPSO_KERNEL_RESIDENT) {
         SwarmIO io{};
         io.rng = randoms;
         io.out_angles = dres;
@@ -463,7 +487,7 @@ ikpso_status ikpso_calculate_pso(float* particles, const float* positions, float
         io.iterations = pso.iterations;
         io.num_swarms = 1;
         IKPSO_HIP(launch_resident(ch, mode, io, s));
-    } else if (family == IKPSO_KERNEL_COOP) {
+    } else if (family_run == IKPSO_KERNEL_COOP) {
         SwarmIO io{};
         io.rng = randoms;
         io.out_angles = dres;
@@ -472,7 +496,7 @@ ikpso_status ikpso_calculate_pso(float* particles, const float* positions, float
         io.P = size;
         io.iterations = pso.iterations;
         io.num_swarms = 1;
-        IKPSO_HIP(carve_coop(io, reinterpret_cast<char*>(dres) + ((head + 255) & ~size_t(255)), cg, cng, D, s));
+        IKPSO_HIP(carve_coop(io, reinterpret_cast<char*>(dres) + ((head + 255) & ~size_t(255)), cg, cng, cblk, D, s));
         IKPSO_HIP(launch_coop(ch, mode, io, s));
         int32_t err = 0;
         IKPSO_HIP(hipMemcpyAsync(result, dres, sizeof(float) * D, hipMemcpyDefault, s));
@@ -554,6 +578,7 @@ ikpso_status ikpso_solver_create(const ikpso_solver_desc* desc, ikpso_solver** o
         s->chain.aux_dev = s->aux;
     }
     s->family = pick_kernel(s->chain, s->mode, s->P, desc->kernel);
+    s->requested = desc->kernel;
     if (s->family < 0 || desc->kernel < IKPSO_KERNEL_AUTO || desc->kernel > IKPSO_KERNEL_COOP) {
         (void)hipFree(s->aux);
         delete s;
@@ -600,7 +625,9 @@ ikpso_status ikpso_solve_batch(ikpso_solver* s, const float* targets, const floa
     if (num_swarms > s->capacity || !s->rng) return IKPSO_ERR_INVALID_ARG;  // seed first
     if (num_swarms > 0x7fffffff) return IKPSO_ERR_INVALID_ARG;
     const hipStream_t hs = (hipStream_t)stream;
-    if (s->family == IKPSO_KERNEL_RESIDENT) {
+    const bool latency_coop = s->family == IKPSO_KERNEL_RESIDENT && s->requested == IKPSO_KERNEL_AUTO &&
+                              prefer_latency_coop(s->chain, s->mode, s->P, num_swarms);
+    if (s->family == IKPSO_KERNEL_RESIDENT && !latency_coop) {
         SwarmIO io{};
         io.targets = targets;
         io.start_pose = start_pose;
@@ -615,9 +642,10 @@ ikpso_status ikpso_solve_batch(ikpso_solver* s, const float* targets, const floa
         return IKPSO_OK;
     }
     const int D = 3 * s->chain.J;
-    if (s->family == IKPSO_KERNEL_COOP) {
-        int G, NG;
-        if (!coop_plan(s->chain, s->mode, s->P, num_swarms, &G, &NG)) return IKPSO_ERR_UNSUPPORTED;
+    if (s->family == IKPSO_KERNEL_COOP || latency_coop) {
+        int G, NG, T;
+        if (!coop_plan(s->chain, s->mode, s->P, num_swarms, s->requested == IKPSO_KERNEL_AUTO, &G, &NG, &T))
+            return IKPSO_ERR_UNSUPPORTED;
         const size_t need = coop_workspace_bytes(NG, G, D);
         if (need > s->ws_bytes) {
             if (s->ws) IKPSO_HIP(hipFree(s->ws));
@@ -636,7 +664,7 @@ ikpso_status ikpso_solve_batch(ikpso_solver* s, const float* targets, const floa
         io.P = s->P;
         io.iterations = iterations;
         io.num_swarms = num_swarms;
-        IKPSO_HIP(carve_coop(io, s->ws, G, NG, D, hs));
+        IKPSO_HIP(carve_coop(io, s->ws, G, NG, T, D, hs));
         IKPSO_HIP(launch_coop(s->chain, s->mode, io, hs));
         return IKPSO_OK;
     }

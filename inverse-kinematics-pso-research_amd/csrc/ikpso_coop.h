@@ -129,13 +129,14 @@ __device__ __forceinline__ void coop_exchange(SwarmShared<J>& sh, CoopShared<J>&
     __syncthreads();
 }
 
-template <class Topo, int MODE, int TERMS>
-__global__ void __launch_bounds__(kCoopThreads<Topo::J>(), kCoopThreads<Topo::J>() / 256)
+// BLOCK: kCoopThreads<J>() (throughput: fill each CU), or kCoopLatencyThreads
+// for a few swarms (latency: one wave per SIMD on 4x more CUs).
+template <class Topo, int MODE, int TERMS, int BLOCK>
+__global__ void __launch_bounds__(BLOCK, (BLOCK >= 256 ? BLOCK / 256 : 1))
     k_swarm_coop(const ChainConsts<Topo::J> cc, const SwarmIO io)
 {
     constexpr int J = Topo::J;
     constexpr int D = 3 * J;
-    constexpr int BLOCK = kCoopThreads<J>();
     const int tid = threadIdx.x;
     const int P = io.P;
 
@@ -235,11 +236,10 @@ __global__ void __launch_bounds__(kCoopThreads<Topo::J>(), kCoopThreads<Topo::J>
 // checked here against the occupancy query (the check hipLaunchCooperativeKernel
 // would make; a plain launch gives the same residency without the cooperative
 // queue): an oversized grid is an error, never a hang.
-template <class Topo, int MODE, int TERMS>
-inline hipError_t launch_coop_kernel(const ChainConsts<Topo::J>& cc, const SwarmIO& io, hipStream_t stream)
+template <class Topo, int MODE, int TERMS, int T>
+inline hipError_t launch_coop_block(const ChainConsts<Topo::J>& cc, const SwarmIO& io, hipStream_t stream)
 {
-    constexpr int T = kCoopThreads<Topo::J>();
-    const auto kernel = &k_swarm_coop<Topo, MODE, TERMS>;
+    const auto kernel = &k_swarm_coop<Topo, MODE, TERMS, T>;
     int dev = 0, cus = 0, per_cu = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
@@ -249,6 +249,17 @@ inline hipError_t launch_coop_kernel(const ChainConsts<Topo::J>& cc, const Swarm
     if (per_cu < 1 || grid > (int64_t)cus) return hipErrorCooperativeLaunchTooLarge;
     hipLaunchKernelGGL(kernel, dim3((unsigned)grid), dim3(T), 0, stream, cc, io);
     return hipGetLastError();
+}
+
+template <class Topo, int MODE, int TERMS>
+inline hipError_t launch_coop_kernel(const ChainConsts<Topo::J>& cc, const SwarmIO& io, hipStream_t stream)
+{
+    if constexpr (kCoopThreads<Topo::J>() != kCoopLatencyThreads) {
+        if (io.coop_block == kCoopLatencyThreads)
+            return launch_coop_block<Topo, MODE, TERMS, kCoopLatencyThreads>(cc, io, stream);
+    }
+    if (io.coop_block != kCoopThreads<Topo::J>()) return hipErrorInvalidValue;
+    return launch_coop_block<Topo, MODE, TERMS, kCoopThreads<Topo::J>()>(cc, io, stream);
 }
 
 template <class Topo, int MODE>

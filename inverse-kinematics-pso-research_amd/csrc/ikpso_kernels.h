@@ -83,7 +83,10 @@ __host__ __device__ constexpr int kCoopThreads()
 // to a 64-B multiple.
 __host__ __device__ constexpr int kCoopSlot(int D) { return ((D + 2 + 15) / 16) * 16; }
 
-constexpr int kCoopCounterStride = 32;  // one 128-B line per group counter
+constexpr int kCoopCounterStride = 32;
+// Latency variant of the cooperative kernel (few swarms, chains of <= 10
+// joints): 256-lane chunks, one wave per SIMD, a swarm of 1024 over 4 CUs.
+constexpr int kCoopLatencyThreads = 256;  // one 128-B line per group counter
 template <int J>
 ChainConsts<J> make_consts(const ChainHost& h)
 {
@@ -133,6 +136,7 @@ hipError_t launch_coop(const ChainHost& ch, int mode, const SwarmIO& io, hipStre
 // Co-resident workgroups per CU of the cooperative kernel, CU count, threads per workgroup.
 struct CoopGeometry {
     int threads = 0, blocks_per_cu = 0, cus = 0;
+    bool latency_variant = false;  // a kCoopLatencyThreads build exists for this chain
 };
 bool coop_geometry(const ChainHost& ch, int mode, CoopGeometry* g);
 size_t coop_workspace_bytes(int ng, int G, int D);

@@ -148,6 +148,7 @@ bool coop_geometry(const ChainHost& ch, int mode, CoopGeometry* g)
         using T = decltype(topo);
         if constexpr (!T::kGeneric) {
             g->threads = kCoopThreads<T::J>();
+            g->latency_variant = kCoopThreads<T::J>() != kCoopLatencyThreads;
             spec = true;
         }
     });

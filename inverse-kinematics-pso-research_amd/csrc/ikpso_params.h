@@ -56,6 +56,8 @@ struct SwarmIO {
     int32_t* coop_error;      // set to 1 if a group wait timed out
     int32_t coop_g;
     int32_t coop_ng;
+    int32_t coop_block;       // workgroup size (kCoopThreads<J>() or kCoopLatencyThreads)
+    int32_t pad_;
 };
 
 // Streaming (state-in-HBM) kernels: one launch per PSO iteration over every

@@ -105,11 +105,19 @@ def run_compat(chain, P, I, arith, seed_base=0, monkeypatch=None, positions=None
     return res, parts.cpu().numpy(), bests.cpu().numpy(), r.cpu().numpy()
 
 
+# AUTO: a single swarm of <= 1024 particles runs the cooperative kernel's
+# latency variant (256-lane chunks on ceil(P/256) CUs); "resident" forces the
+# one-workgroup kernel the batched throughput path uses.
+KERNELS = ["resident", "auto"]
+
+
+@pytest.mark.parametrize("kernel", KERNELS)
 @pytest.mark.parametrize("arith", ["fast", "reference"])
 @pytest.mark.parametrize("P", [1, 65, 256, 1024])
-def test_calculate_pso_init_is_exact(oracle, device, scene_chain, monkeypatch, arith, P):
+def test_calculate_pso_init_is_exact(oracle, device, scene_chain, monkeypatch, arith, P, kernel):
     """I = 0: warm start, velocity draws, pbest, argmin, result and generator states."""
     monkeypatch.setenv("IKPSO_ARITH", arith)
+    monkeypatch.setenv("IKPSO_KERNEL", kernel)
     res, parts, bests, r = run_compat(scene_chain, P, 0, arith)
     ostate = oracle.init_generators(P, 0)
     ores, oparts, obests = oracle.calculate_pso(scene_chain, P, ostate, iterations=0)
@@ -133,10 +141,12 @@ def test_calculate_pso_one_step(oracle, device, scene_chain, monkeypatch, arith)
     assert np.max(np.abs(bests - obests) / obests) < 1e-5
 
 
+@pytest.mark.parametrize("kernel", KERNELS)
 @pytest.mark.parametrize("arith", ["fast", "reference"])
-@pytest.mark.parametrize("P,I", [(256, 20), (1024, 20)])
-def test_tier_a(oracle, device, scene_chain, monkeypatch, arith, P, I):
+@pytest.mark.parametrize("P,I", [(256, 20), (1024, 20), (700, 13)])
+def test_tier_a(oracle, device, scene_chain, monkeypatch, arith, P, I, kernel):
     monkeypatch.setenv("IKPSO_ARITH", arith)
+    monkeypatch.setenv("IKPSO_KERNEL", kernel)
     res, parts, bests, r = run_compat(scene_chain, P, I, arith)
     ostate = oracle.init_generators(P, 0)
     ores, oparts, obests = oracle.calculate_pso(scene_chain, P, ostate, iterations=I)
@@ -213,9 +223,11 @@ def batch_case(oracle):
     return wl, B, P, I, tg, oang, ofit, ores
 
 
-def test_batch_vs_oracle(device, batch_case):
+@pytest.mark.parametrize("kernel", ["resident", "auto"])
+def test_batch_vs_oracle(device, batch_case, kernel):
+    """24 swarms: AUTO takes the cooperative latency variant (4 CUs per swarm)."""
     wl, B, P, I, tg, oang, ofit, ores = batch_case
-    s = ikpso.BatchSolver(wl.chain, P, pso=wl.pso)
+    s = ikpso.BatchSolver(wl.chain, P, pso=wl.pso, kernel=kernel)
     s.seed(B)
     ang, fit, res = s.solve(dev(tg), iterations=I)
     ang, fit, res = ang.cpu().numpy(), fit.cpu().numpy(), res.cpu().numpy()
