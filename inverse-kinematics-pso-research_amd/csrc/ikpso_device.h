@@ -19,6 +19,9 @@
 #ifndef IKPSO_SINCOS_V2
 #define IKPSO_SINCOS_V2 1
 #endif
+#ifndef IKPSO_FK_SEQ
+#define IKPSO_FK_SEQ 1
+#endif
 #ifndef IKPSO_CLAMP_MED3
 #define IKPSO_CLAMP_MED3 1
 #endif
@@ -228,6 +231,7 @@ struct TopoRef7 {
     static constexpr int J = 7;
     static constexpr bool kGeneric = false;
     __host__ __device__ static constexpr int parent(int k) { return k <= 5 ? k - 1 : 4; }
+    __host__ __device__ static constexpr bool leaf(int k) { return k >= 5; }  // no child reads its frame
     __host__ __device__ static constexpr bool effector(int k) { return k >= 5; }
 };
 
@@ -237,6 +241,7 @@ struct TopoSerialTip {
     static constexpr int J = J_;
     static constexpr bool kGeneric = false;
     __host__ __device__ static constexpr int parent(int k) { return k - 1; }
+    __host__ __device__ static constexpr bool leaf(int k) { return k == J_; }
     __host__ __device__ static constexpr bool effector(int k) { return k == J_; }
 };
 
@@ -247,6 +252,7 @@ struct TopoGeneric {
     static constexpr int J = J_;
     static constexpr bool kGeneric = true;
     __host__ __device__ static constexpr int parent(int k) { return k - 1; }  // unused
+    __host__ __device__ static constexpr bool leaf(int) { return false; }
     __host__ __device__ static constexpr bool effector(int) { return true; }
 };
 
@@ -289,6 +295,42 @@ __device__ __forceinline__ Frame child_frame_fast(const Frame& P, float a, float
     W.r20 = P.r20 * l00 + P.r21 * l10 + P.r22 * l20;
     W.r21 = P.r20 * l01 + P.r21 * l11 + P.r22 * l21;
     W.r22 = P.r20 * l02 + P.r21 * l12 + P.r22 * l22;
+    W.px = P.px + len * W.r00;
+    W.py = P.py + len * W.r10;
+    W.pz = P.pz + len * W.r20;
+    return W;
+}
+
+// FAST, interior nodes (the whole world rotation is consumed by the children):
+// apply Rx, Ry, Rz to the parent's columns in turn -- each is a plane rotation
+// of two columns (12 multiply-adds), 36 in all against 14 + 27 for building
+// the local matrix and multiplying it in.  Leaves, which only need the first
+// column, keep the closed form (the compiler then drops the other columns).
+__device__ __forceinline__ Frame child_frame_fast_seq(const Frame& P, float a, float b, float c, float len)
+{
+    float sa, ca, sb, cb, sc, cc;
+    sincos_fast(a, &sa, &ca);
+    sincos_fast(b, &sb, &cb);
+    sincos_fast(c, &sc, &cc);
+    // * Rx(a): columns 1, 2 become (ca c1 + sa c2, ca c2 - sa c1)
+    const float x01 = P.r01 * ca + P.r02 * sa, x02 = P.r02 * ca - P.r01 * sa;
+    const float x11 = P.r11 * ca + P.r12 * sa, x12 = P.r12 * ca - P.r11 * sa;
+    const float x21 = P.r21 * ca + P.r22 * sa, x22 = P.r22 * ca - P.r21 * sa;
+    // * Ry(b): columns 0, 2 become (cb c0 - sb c2, sb c0 + cb c2)
+    const float y00 = P.r00 * cb - x02 * sb, y02 = P.r00 * sb + x02 * cb;
+    const float y10 = P.r10 * cb - x12 * sb, y12 = P.r10 * sb + x12 * cb;
+    const float y20 = P.r20 * cb - x22 * sb, y22 = P.r20 * sb + x22 * cb;
+    // * Rz(c): columns 0, 1 become (cc c0 + sc c1, cc c1 - sc c0)
+    Frame W;
+    W.r00 = y00 * cc + x01 * sc;
+    W.r01 = x01 * cc - y00 * sc;
+    W.r02 = y02;
+    W.r10 = y10 * cc + x11 * sc;
+    W.r11 = x11 * cc - y10 * sc;
+    W.r12 = y12;
+    W.r20 = y20 * cc + x21 * sc;
+    W.r21 = x21 * cc - y20 * sc;
+    W.r22 = y22;
     W.px = P.px + len * W.r00;
     W.py = P.py + len * W.r10;
     W.pz = P.pz + len * W.r20;
@@ -338,11 +380,15 @@ __device__ __forceinline__ Frame child_frame_reference(const Frame& P, float a, 
     return W;
 }
 
-template <int MODE>
+// SEQ: FAST mode may compose the rotation column-wise (interior nodes, or any
+// node whose full frame is consumed).
+template <int MODE, bool SEQ = false>
 __device__ __forceinline__ Frame child_frame(const Frame& P, float a, float b, float c, float len)
 {
     if constexpr (MODE == IKPSO_ARITH_REFERENCE)
         return child_frame_reference(P, a, b, c, len);
+    else if constexpr (SEQ && IKPSO_FK_SEQ)
+        return child_frame_fast_seq(P, a, b, c, len);
     else
         return child_frame_fast(P, a, b, c, len);
 }
@@ -387,7 +433,11 @@ struct FitnessAcc {
     {
 #pragma clang fp contract(off)
         const int pk = Topo::kGeneric ? cc.parent[k] : Topo::parent(k);
-        F[k] = child_frame<MODE>(F[pk], a, b, c, cc.len[k]);
+        // column-wise composition unless only the leaf's position is consumed
+        if (!Topo::kGeneric && (!Topo::leaf(k) || (TERMS & kTermColliders)))
+            F[k] = child_frame<MODE, true>(F[pk], a, b, c, cc.len[k]);
+        else
+            F[k] = child_frame<MODE>(F[pk], a, b, c, cc.len[k]);
         const float dx = rest3[0] - a, dy = rest3[1] - b, dz = rest3[2] - c;
         if constexpr (MODE == IKPSO_ARITH_REFERENCE) {
             rot_diff = rot_diff + ((dx * dx + dy * dy) + dz * dz);
