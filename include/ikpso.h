@@ -191,7 +191,13 @@ ikpso_status ikpso_solver_seed(ikpso_solver* solver, int64_t capacity, uint64_t 
  *   start_pose device, [B][D] or NULL (NULL: chain rotations).
  *   out_angles device [B][D]; out_fitness device [B]; out_residual device [B] or NULL
  *   (residual = sum over effectors of |p_e - t_e|, as checkDistance).
- * Stream-ordered; does not synchronise. */
+ * Stream-ordered; does not synchronise.  A solver handle owns one workspace:
+ * calls on one handle must be ordered (one stream, or synchronised), not
+ * concurrent.  The cooperative family needs its workgroups co-resident (one per
+ * CU): the grid is checked against the occupancy query at launch, and if other
+ * work on the device still keeps a group from assembling, its bounded wait
+ * gives up and the swarms it had not finished get a NaN fitness (never a
+ * hang); ikpso_calculate_pso reports this as IKPSO_ERR_HIP. */
 ikpso_status ikpso_solve_batch(ikpso_solver* solver, const float* targets, const float* start_pose,
                                int64_t num_swarms, int32_t iterations, float* out_angles, float* out_fitness,
                                float* out_residual, void* stream);
