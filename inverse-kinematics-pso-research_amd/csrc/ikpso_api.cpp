@@ -372,6 +372,7 @@ struct ikpso_solver {
     float* aux = nullptr;  // device copy of chain.aux
     int family = IKPSO_KERNEL_RESIDENT;
     int requested = IKPSO_KERNEL_AUTO;
+    std::string kname;     // kernel family / topology, for ikpso_solver_kernel_name
     void* ws = nullptr;    // streaming / cooperative workspace
     size_t ws_bytes = 0;
     int P = 0;
@@ -579,6 +580,7 @@ ikpso_status ikpso_solver_create(const ikpso_solver_desc* desc, ikpso_solver** o
     }
     s->family = pick_kernel(s->chain, s->mode, s->P, desc->kernel);
     s->requested = desc->kernel;
+    if (s->family >= 0) s->kname = kernel_name(s->chain, s->family);
     if (s->family < 0 || desc->kernel < IKPSO_KERNEL_AUTO || desc->kernel > IKPSO_KERNEL_COOP) {
         (void)hipFree(s->aux);
         delete s;
@@ -701,7 +703,7 @@ int ikpso_solver_dof(const ikpso_solver* s) { return s ? 3 * s->chain.J : 0; }
 int ikpso_solver_effectors(const ikpso_solver* s) { return s ? s->chain.E : 0; }
 const char* ikpso_solver_kernel_name(const ikpso_solver* s)
 {
-    return s ? kernel_name(s->chain, s->family) : "";
+    return s ? s->kname.c_str() : "";
 }
 
 }  // extern "C"

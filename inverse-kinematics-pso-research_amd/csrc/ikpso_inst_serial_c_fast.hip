@@ -1,0 +1,11 @@
+// ikpso_inst_serial_c_fast.hip -- kernel instantiations for serial chains of 12, 13, 14 joints with a tip
+// effector (DH arms built by ikpso.dh).
+#include "ikpso_topo_impl.h"
+
+namespace ikpso {
+#if IKPSO_WITH_OTHERS
+template struct ModeOps<TopoSerialTip<12>, IKPSO_ARITH_FAST>;
+template struct ModeOps<TopoSerialTip<13>, IKPSO_ARITH_FAST>;
+template struct ModeOps<TopoSerialTip<14>, IKPSO_ARITH_FAST>;
+#endif
+}  // namespace ikpso

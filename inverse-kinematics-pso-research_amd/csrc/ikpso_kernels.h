@@ -6,6 +6,7 @@
 
 #include <string.h>
 
+#include <string>
 #include <vector>
 
 #include "ikpso.h"
@@ -142,6 +143,6 @@ bool coop_geometry(const ChainHost& ch, int mode, CoopGeometry* g);
 size_t coop_workspace_bytes(int ng, int G, int D);
 int resident_max_threads(const ChainHost& ch);
 bool chain_supported(const ChainHost& ch);
-const char* kernel_name(const ChainHost& ch, int family);  // IKPSO_KERNEL_*
+std::string kernel_name(const ChainHost& ch, int family);  // IKPSO_KERNEL_*
 
 }  // namespace ikpso

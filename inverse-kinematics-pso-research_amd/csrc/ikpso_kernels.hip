@@ -13,6 +13,7 @@
 //     (randInitKernel, src/utility_kernels.cuh:21-31).
 #include <hip/hip_runtime.h>
 
+#include <string>
 #include <type_traits>
 
 #include "ikpso_device.h"
@@ -69,33 +70,20 @@ bool chain_supported(const ChainHost& ch)
     return visit_topology(ch, [](auto) {});
 }
 
-const char* kernel_name(const ChainHost& ch, int family)
+std::string kernel_name(const ChainHost& ch, int family)
 {
-    const bool streaming = family == IKPSO_KERNEL_STREAMING;
-    if (family == IKPSO_KERNEL_COOP) {
-        const char* name = "swarm_coop<generic>";
-        visit_topology(ch, [&](auto topo) {
-            using T = decltype(topo);
-            if constexpr (std::is_same_v<T, TopoRef7>) name = "swarm_coop<ref_tree7>";
-            else if constexpr (std::is_same_v<T, TopoSerialTip<6>>) name = "swarm_coop<serial_tip6>";
-            else if constexpr (std::is_same_v<T, TopoSerialTip<7>>) name = "swarm_coop<serial_tip7>";
-            else if constexpr (std::is_same_v<T, TopoSerialTip<20>>) name = "swarm_coop<serial_tip20>";
-        });
-        return name;
-    }
-    const char* name = streaming ? "swarm_streaming<generic>" : "swarm_resident<generic>";
-    visit_topology(ch, [&](auto topo) {
-        using T = decltype(topo);
+    const char* fam = family == IKPSO_KERNEL_COOP ? "swarm_coop" : family == IKPSO_KERNEL_STREAMING
+                                                                       ? "swarm_streaming"
+                                                                       : "swarm_resident";
+    std::string topo = "generic";
+    visit_topology(ch, [&](auto t) {
+        using T = decltype(t);
         if constexpr (std::is_same_v<T, TopoRef7>)
-            name = streaming ? "swarm_streaming<ref_tree7>" : "swarm_resident<ref_tree7>";
-        else if constexpr (std::is_same_v<T, TopoSerialTip<6>>)
-            name = streaming ? "swarm_streaming<serial_tip6>" : "swarm_resident<serial_tip6>";
-        else if constexpr (std::is_same_v<T, TopoSerialTip<7>>)
-            name = streaming ? "swarm_streaming<serial_tip7>" : "swarm_resident<serial_tip7>";
-        else if constexpr (std::is_same_v<T, TopoSerialTip<20>>)
-            name = streaming ? "swarm_streaming<serial_tip20>" : "swarm_resident<serial_tip20>";
+            topo = "ref_tree7";
+        else if constexpr (!T::kGeneric)
+            topo = "serial_tip" + std::to_string(T::J);
     });
-    return name;
+    return std::string(fam) + "<" + topo + ">";
 }
 
 hipError_t launch_resident(const ChainHost& ch, int mode, const SwarmIO& io, hipStream_t stream)

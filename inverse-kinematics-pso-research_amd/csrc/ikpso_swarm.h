@@ -157,10 +157,12 @@ inline bool visit_topology(const ChainHost& ch, F&& f)
         break;
 #endif
     case TopoKind::SerialTip:
-        switch (ch.J) {  // common arm lengths (6- and 7-joint DH arms) and BASELINE config 5
+        switch (ch.J) {  // arm lengths of DH arms (6-14 nodes: 6-7 joints + d offsets) and BASELINE config 5
 #if IKPSO_WITH_OTHERS
-        case 6: f(TopoSerialTip<6>{}); return true;
-        case 7: f(TopoSerialTip<7>{}); return true;
+#define IKPSO_S(n) \
+    case n: f(TopoSerialTip<n>{}); return true;
+            IKPSO_S(6) IKPSO_S(7) IKPSO_S(8) IKPSO_S(9) IKPSO_S(10) IKPSO_S(11) IKPSO_S(12) IKPSO_S(13) IKPSO_S(14)
+#undef IKPSO_S
 #endif
 #if IKPSO_WITH_SERIAL20
         case 20: f(TopoSerialTip<20>{}); return true;

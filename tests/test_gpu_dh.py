@@ -30,7 +30,7 @@ def reachable_targets(arm_spec, n, rng):
     return np.array([dh_forward(t, arm_spec["d"], arm_spec["a"], arm_spec["alpha"]) for t in th], np.float32)
 
 
-@pytest.mark.parametrize("spec,kern", [(IIWA, "generic"), (PLANARISH, "serial_tip7")])
+@pytest.mark.parametrize("spec,kern", [(IIWA, "serial_tip11"), (PLANARISH, "serial_tip7")])
 def test_dh_reference_bitexact(oracle, device, spec, kern):
     arm = dh_arm(spec["a"], spec["alpha"], spec["d"], -LIM, LIM)
     chain = arm.origin.to_cuda()
@@ -58,6 +58,8 @@ def test_dh_solves_reachable_targets(device, spec):
     tg = reachable_targets(spec, B, rng)
     fit_cfg = ikpso.FitnessConfig(0.0, 0.0, 0.1)  # position only: no pull towards the rest pose
     s = ikpso.BatchSolver(chain, 1024, pso=ikpso.PSOConfig(0.5, 0.5, 1.25, 400), fit=fit_cfg)
+    # 7 nodes: one workgroup per swarm; 11 nodes (iiwa: 4 d offsets): two 512-lane chunks per swarm
+    assert ("resident" if len(chain) == 8 else "coop") in s.kernel
     s.seed(B)
     ang, fit, res = (t.cpu().numpy() for t in s.solve(dev(tg.reshape(B, 1, 3)), iterations=400))
     s.close()
