@@ -87,8 +87,16 @@ def cpu_baseline(wl, seconds: float, threads: int):
         if el >= seconds or done >= 64 * threads:
             break
     ups = done * P * I / el
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
     return {"value": ups, "unit": "particle-updates/s", "cores": threads, "kind": "port",
-            "solves_per_s": done / el,
+            "solves_per_s": done / el, "cpu_model": model, "host_cpus": os.cpu_count(),
             "sample": f"{done} swarms x {P} particles x {I} iterations of config 3 (same targets/seeds), "
                       f"OpenMP over swarms, {el:.1f} s"}
 
