@@ -85,9 +85,12 @@ __host__ __device__ constexpr int kCoopThreads()
 __host__ __device__ constexpr int kCoopSlot(int D) { return ((D + 2 + 15) / 16) * 16; }
 
 constexpr int kCoopCounterStride = 32;
-// Latency variant of the cooperative kernel (few swarms, chains of <= 10
-// joints): 256-lane chunks, one wave per SIMD, a swarm of 1024 over 4 CUs.
-constexpr int kCoopLatencyThreads = 256;  // one 128-B line per group counter
+// Latency variant of the cooperative kernel (few swarms): 256-lane chunks,
+// one wave per SIMD, a swarm of 1024 over 4 CUs.
+#ifndef IKPSO_COOP_LATENCY_THREADS
+#define IKPSO_COOP_LATENCY_THREADS 256
+#endif
+constexpr int kCoopLatencyThreads = IKPSO_COOP_LATENCY_THREADS;
 template <int J>
 ChainConsts<J> make_consts(const ChainHost& h)
 {
