@@ -87,6 +87,10 @@ def cpu_baseline(wl, seconds: float, threads: int):
         if el >= seconds or done >= 64 * threads:
             break
     ups = done * P * I / el
+    # one thread, one swarm of the same workload (1 thread and all cores)
+    t1 = time.perf_counter()
+    oracle.solve_batch(wl.chain, wl.targets(first, 1), None, P, I, oracle.init_generators(P, first * P), threads=1)
+    ups1 = P * I / (time.perf_counter() - t1)
     model = None
     try:
         for line in open("/proc/cpuinfo"):
@@ -96,7 +100,7 @@ def cpu_baseline(wl, seconds: float, threads: int):
     except OSError:
         pass
     return {"value": ups, "unit": "particle-updates/s", "cores": threads, "kind": "port",
-            "solves_per_s": done / el, "cpu_model": model, "host_cpus": os.cpu_count(),
+            "solves_per_s": done / el, "value_1thread": ups1, "cpu_model": model, "host_cpus": os.cpu_count(),
             "sample": f"{done} swarms x {P} particles x {I} iterations of config 3 (same targets/seeds), "
                       f"OpenMP over swarms, {el:.1f} s"}
 
