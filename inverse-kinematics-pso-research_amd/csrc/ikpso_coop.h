@@ -32,6 +32,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "ikpso_resident.h"
 
 namespace ikpso {
@@ -168,7 +170,10 @@ __global__ void __launch_bounds__(BLOCK, (BLOCK >= 256 ? BLOCK / 256 : 1))
         if (b >= io.num_swarms) break;
         const int i = cs.member * BLOCK + tid;  // particle index within the swarm
         stage_swarm_inputs<J>(cc, io.targets, io.start_pose, b, sh);
-        Xorwow rng{0, 0, 0, 0, 0, 0};
+        // the add-for-shift issue form only in the latency variant (one wave per
+        // SIMD, room to spare): in the 2-wave serial-20 kernel it cost 5 %
+        using Rng = XorwowT<(BLOCK == kCoopLatencyThreads) && std::is_same_v<RngFor<TERMS>, XorwowT<true>>>;
+        Rng rng{0, 0, 0, 0, 0, 0};
         if (i < P) load_rng(rng, io.rng + b * P + i);
         if (tid == 0) cs.gkey = 0xFFFFFFFFu;
         __syncthreads();

@@ -31,6 +31,21 @@
 #ifndef IKPSO_SCHED_DIM
 #define IKPSO_SCHED_DIM 1
 #endif
+// gfx950 VALU issue costs (tools/probes/valu_probe.hip, 4 waves per SIMD):
+// a wave64 v_add_u32 / v_xor_b32 / v_bitop3_b32 / v_fma_f32 on VGPR, inline or
+// literal operands issues every ~2.1-2.5 cycles per SIMD, but every
+// v_lshlrev_b32 and every VALU op that reads an SGPR takes ~4.1.  So t << 1 is
+// issued as t + t, and the sincos sign mask and the FAST-mode PSO coefficients
+// are held in VGPRs.
+#ifndef IKPSO_ISSUE_SHL1_ADD
+#define IKPSO_ISSUE_SHL1_ADD 1
+#endif
+#ifndef IKPSO_ISSUE_SIGN_VGPR
+#define IKPSO_ISSUE_SIGN_VGPR 0
+#endif
+#ifndef IKPSO_ISSUE_COEF_VGPR
+#define IKPSO_ISSUE_COEF_VGPR 0
+#endif
 
 namespace ikpso {
 
@@ -47,11 +62,40 @@ __host__ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32
 #endif
 }
 
+// t << 1 as t + t (v_add_u32 issues twice as fast as v_lshlrev_b32; opaque to
+// the compiler, which would canonicalise an add back into the shift).
+__host__ __device__ __forceinline__ uint32_t shl1(uint32_t t)
+{
+#if defined(__HIP_DEVICE_COMPILE__) && IKPSO_ISSUE_SHL1_ADD
+    uint32_t r;
+    asm("v_add_u32 %0, %1, %1" : "=v"(r) : "v"(t));
+    return r;
+#else
+    return t << 1;
+#endif
+}
+
+// A wave-uniform 32-bit value copied into a VGPR, so that the VALU ops reading
+// it do not take the SGPR-operand issue cost.
+__device__ __forceinline__ uint32_t to_vgpr(uint32_t s)
+{
+    uint32_t r;
+    asm("v_mov_b32 %0, %1" : "=v"(r) : "s"(s));
+    return r;
+}
+__device__ __forceinline__ float to_vgpr(float s) { return __uint_as_float(to_vgpr(__float_as_uint(s))); }
+
 // a ^ (b & 0x80000000): flip the sign of the float bits a where b's top bit is set.
 __host__ __device__ __forceinline__ uint32_t xor_sign(uint32_t a, uint32_t b)
 {
 #if defined(__HIP_DEVICE_COMPILE__)
+#if IKPSO_ISSUE_SIGN_VGPR
+    uint32_t m;
+    asm("v_mov_b32 %0, 0x80000000" : "=v"(m));
+    return __builtin_amdgcn_bitop3_b32(a, b, m, 0x78);
+#else
     return __builtin_amdgcn_bitop3_b32(a, b, 0x80000000u, 0x78);
+#endif
 #else
     return a ^ (b & 0x80000000u);
 #endif
@@ -72,7 +116,9 @@ __host__ __device__ __forceinline__ uint32_t as_uint(float f)
 
 // ---------------------------------------------------------------- XORWOW
 // cuRAND XORWOW restated: state {d, v[5]}; curand() and curand_uniform().
-struct Xorwow {
+// kAddShl: issue t << 1 as t + t (see IKPSO_ISSUE_SHL1_ADD; same bits).
+template <bool kAddShl>
+struct XorwowT {
     uint32_t d, v0, v1, v2, v3, v4;
 
     __host__ __device__ __forceinline__ uint32_t next()
@@ -82,7 +128,7 @@ struct Xorwow {
         v1 = v2;
         v2 = v3;
         v3 = v4;
-        v4 = xor3(v4, v4 << 4, t) ^ (t << 1);  // (v4 ^ (v4 << 4)) ^ (t ^ (t << 1))
+        v4 = xor3(v4, v4 << 4, t) ^ (kAddShl ? shl1(t) : t << 1);  // (v4 ^ (v4 << 4)) ^ (t ^ (t << 1))
         d += 362437u;
         return v4 + d;
     }
@@ -108,6 +154,7 @@ struct Xorwow {
 #endif
     }
 };
+using Xorwow = XorwowT<false>;
 
 __host__ __device__ inline void xorwow_seed(uint64_t seed, uint32_t st[6])
 {
@@ -411,6 +458,16 @@ __device__ __forceinline__ Frame child_frame(const Frame& P, float a, float b, f
 // (src/kernel.cu:104-136), compiled in only when the scene has colliders.
 constexpr int kTermPosRef = 1, kTermPenalty = 2, kTermRuntime = 4, kTermUniformBounds = 8, kTermColliders = 16;
 
+// Generator type of a swarm kernel: the add-for-shift issue form everywhere but
+// in the collider kernels, whose register allocation the opaque add perturbs
+// (spills); the draws are bit-identical either way.
+template <int TERMS>
+using RngFor = XorwowT<IKPSO_ISSUE_SHL1_ADD != 0 && !(TERMS & kTermColliders)>;
+// FAST-mode PSO coefficients in VGPRs: only the resident kernel's specialised
+// (uniform-bounds) instantiations have the registers for it.
+template <int TERMS>
+constexpr bool kCoefVgpr = IKPSO_ISSUE_COEF_VGPR != 0 && (TERMS & kTermUniformBounds) && !(TERMS & kTermColliders);
+
 template <class Topo, int MODE, int TERMS>
 struct FitnessAcc {
     static constexpr int J = Topo::J;
@@ -548,10 +605,14 @@ struct PsoCoef {
     float wh, c1h, c2h;  // c * 2^-33
 };
 
-template <class CC>
+template <bool kVgpr = false, class CC>
 __device__ __forceinline__ PsoCoef pso_coef(const CC& cc)
 {
-    return PsoCoef{cc.w, cc.c1, cc.c2, cc.wq, cc.c1q, cc.c2q, cc.wh, cc.c1h, cc.c2h};
+    if constexpr (kVgpr)  // FAST mode's folded coefficients feed one FMA per draw
+        return PsoCoef{cc.w, cc.c1, cc.c2, to_vgpr(cc.wq), to_vgpr(cc.c1q), to_vgpr(cc.c2q),
+                       to_vgpr(cc.wh), to_vgpr(cc.c1h), to_vgpr(cc.c2h)};
+    else
+        return PsoCoef{cc.w, cc.c1, cc.c2, cc.wq, cc.c1q, cc.c2q, cc.wh, cc.c1h, cc.c2h};
 }
 
 // simulateParticlesKernel body for one dimension (src/kernel.cu:160-169):
@@ -560,8 +621,8 @@ __device__ __forceinline__ PsoCoef pso_coef(const CC& cc)
 // coefficient into its uniform's affine map, c*r = c*(u*2^-32 + 2^-33) =
 // fma(u, c*2^-32, c*2^-33): one rounding where the reference has two (and
 // three fewer multiplies per dimension).
-template <int MODE>
-__device__ __forceinline__ void pso_update(float& x, float& v, float pb, float g, const PsoCoef& k, Xorwow& rng)
+template <int MODE, class Rng>
+__device__ __forceinline__ void pso_update(float& x, float& v, float pb, float g, const PsoCoef& k, Rng& rng)
 {
     if constexpr (MODE == IKPSO_ARITH_REFERENCE) {
         const float r1 = rng.uniform();

@@ -31,10 +31,10 @@ namespace ikpso {
 // reference's update-all-then-evaluate values in the same order.  The
 // node's LDS operands (local best, global best, rest pose, target) are
 // loaded one node ahead so their latency hides under the previous node.
-template <class Topo, int MODE, int TERMS, int BLOCK>
+template <class Topo, int MODE, int TERMS, int BLOCK, class Rng>
 __device__ __forceinline__ void swarm_step(const ChainConsts<Topo::J>& cc, SwarmShared<Topo::J>& sh, float* s_pb,
                                            int tid, float (&x)[3 * Topo::J], float (&v)[3 * Topo::J], float& pbf,
-                                           const PsoCoef& coef, Xorwow& rng)
+                                           const PsoCoef& coef, Rng& rng)
 {
     constexpr int J = Topo::J;
     constexpr int D = 3 * J;
@@ -110,7 +110,7 @@ __global__ void __launch_bounds__(kResidentMaxThreads<Topo::J>())
     __shared__ float s_pb[D * BLOCK];
     stage_swarm_inputs<J>(cc, io.targets, io.start_pose, b, sh);
 
-    Xorwow rng{0, 0, 0, 0, 0, 0};
+    RngFor<TERMS> rng{0, 0, 0, 0, 0, 0};
     if (active) load_rng(rng, io.rng + b * P + tid);
     __syncthreads();
 
@@ -132,7 +132,7 @@ __global__ void __launch_bounds__(kResidentMaxThreads<Topo::J>())
     copy_gbest<J, BLOCK>(sh, s_pb, bidx);
     __syncthreads();
 
-    const PsoCoef coef = pso_coef(cc);
+    const PsoCoef coef = pso_coef<kCoefVgpr<TERMS>>(cc);
     for (int it = 0; it < io.iterations; ++it) {
         compiler_fence();
         swarm_step<Topo, MODE, TERMS, BLOCK>(cc, sh, s_pb, tid, x, v, pbf, coef, rng);

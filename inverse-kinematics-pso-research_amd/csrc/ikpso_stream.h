@@ -107,7 +107,7 @@ __global__ void __launch_bounds__(kStreamChunk) k_stream_init(const ChainConsts<
     float pbf = 0.0f;
     if (active) {
         // initParticlesKernel (src/kernel.cu:223-266) + initLocalBests (:191-200)
-        Xorwow rng;
+        RngFor<TERMS> rng;
         load_rng(rng, io.rng_aos + b * P + i);
 #pragma unroll
         for (int d = 0; d < D; ++d) {
@@ -149,7 +149,7 @@ __global__ void __launch_bounds__(kStreamChunk) k_stream_step(const ChainConsts<
     float pbf = 0.0f;
     if (active) {
         const int64_t n = io.num_swarms * P, k = b * P + i;
-        Xorwow rng;
+        RngFor<TERMS> rng;
         rng.d = io.rng[0 * n + k];
         rng.v0 = io.rng[1 * n + k];
         rng.v1 = io.rng[2 * n + k];

@@ -10,7 +10,8 @@
 
 namespace ikpso {
 
-__device__ __forceinline__ void load_rng(Xorwow& r, const ikpso_rng_state* p)
+template <class Rng>
+__device__ __forceinline__ void load_rng(Rng& r, const ikpso_rng_state* p)
 {
     const uint32_t* q = reinterpret_cast<const uint32_t*>(p);
     r.d = q[0];
@@ -21,7 +22,8 @@ __device__ __forceinline__ void load_rng(Xorwow& r, const ikpso_rng_state* p)
     r.v4 = q[5];
 }
 
-__device__ __forceinline__ void store_rng(const Xorwow& r, ikpso_rng_state* p)
+template <class Rng>
+__device__ __forceinline__ void store_rng(const Rng& r, ikpso_rng_state* p)
 {
     uint32_t* q = reinterpret_cast<uint32_t*>(p);
     q[0] = r.d;
