@@ -267,6 +267,7 @@ def main():
         print(json.dumps(line), flush=True)
     solver.close()
     if world > 1:
+        dist.barrier()  # rank 0's extra timing runs finish before any rank tears down
         dist.destroy_process_group()
 
 
