@@ -48,6 +48,8 @@ def parse():
                     help="kernel family (auto: resident if the swarm fits one workgroup, else cooperative)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU baseline sample (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
+                    help="gloo: rehearse the N>1 path with ranks sharing the visible GPUs (not a measurement)")
     return ap.parse_args()
 
 
@@ -117,7 +119,10 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    if world > 1 and args.dist_backend == "gloo":
+        torch.cuda.set_device(local % torch.cuda.device_count())
+        dist.init_process_group("gloo")
+    elif world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     else:
@@ -171,7 +176,8 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
-    t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
+    t = torch.tensor([elapsed, kern_ms], dtype=torch.float64,
+                     device="cpu" if args.dist_backend == "gloo" else dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed, kern_ms = float(t[0]), float(t[1])
@@ -252,7 +258,8 @@ def main():
                 "workload": f"config{args.config}: {wl.description}; {P} particles, {I} PSO iterations, "
                             f"{Bl} targets per GPU ({total} total)",
                 "swarms_per_gpu": Bl, "total_swarms": total, "particles": P, "iterations": I, "dof": D,
-                "parallelism": f"dp{world} (swarm shards) + RCCL all-gather of results" if world > 1
+                "parallelism": f"dp{world} (swarm shards) + {'RCCL' if args.dist_backend == 'nccl' else 'gloo (rehearsal)'}"
+                               f" all-gather of results" if world > 1
                 else "1 GPU",
                 "arith": args.arith,
             },

@@ -43,10 +43,11 @@ def gather_rows(local, total: int, world: int, group=None):
     cap = max(counts)
     buf = torch.zeros((cap, cols), dtype=local.dtype, device=local.device)
     buf[: local.shape[0]] = local
-    if dist.get_backend(group) == "gloo":
-        parts = [torch.empty_like(buf) for _ in range(world)]
-        dist.all_gather(parts, buf, group=group)
-        out = torch.cat(parts, dim=0)
+    if dist.get_backend(group) == "gloo":  # host tensors (CPU runs, or a GPU rehearsal over gloo)
+        host = buf.cpu()
+        parts = [torch.empty_like(host) for _ in range(world)]
+        dist.all_gather(parts, host, group=group)
+        out = torch.cat(parts, dim=0).to(local.device)
     else:
         out = torch.empty((cap * world, cols), dtype=local.dtype, device=local.device)
         dist.all_gather_into_tensor(out, buf, group=group)
