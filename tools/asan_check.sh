@@ -1,0 +1,34 @@
+#!/bin/bash
+# Host-code AddressSanitizer + UBSan run of the library's C/C++ side (argument
+# checking, chain parsing, workspace carving, the reference-signature entry
+# points: ikpso_api.cpp, ikpso_compat.cpp) and of the two caller examples.
+# Device code is not instrumented (GPU ASan is not available on this pool), and
+# the kernel translation units are built without it: instrumenting their host
+# side left the 1024-lane kernels' launches returning success without running.
+#   tools/asan_check.sh build   -- here (CPU): builds variants/asan/
+#   tools/asan_check.sh run     -- on the GPU box
+set -e
+ROOT="$(cd "$(dirname "$0")/.." && pwd)"
+OUT="$ROOT/variants/asan"
+RT="$(dirname "$(/opt/rocm/llvm/bin/clang -print-file-name=libclang_rt.asan-x86_64.so 2>/dev/null)")"
+[ -d "$RT" ] || RT=/opt/rocm/llvm/lib/clang/22/lib/linux
+SAN="-Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined -Xarch_host -fno-omit-frame-pointer"
+case "$1" in
+build)
+  mkdir -p "$OUT"
+  make -s -C "$ROOT/inverse-kinematics-pso-research_amd/csrc" -j8 OUT="$OUT/libikpso.so" BUILD=_build_asan \
+       EXTRA="-DIKPSO_EXPERIMENT_REF7_ONLY" CPPEXTRA="$SAN" LDEXTRA="-fsanitize=address,undefined -shared-libsan -Wl,-rpath,$RT"
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 $SAN -O1 -std=c++17 -I"$ROOT/include" "$ROOT/examples/compat_frames.cpp" \
+       -o "$OUT/compat_frames" -L"$OUT" -likpso -Wl,-rpath,'$ORIGIN' -Wl,-rpath,$RT -fsanitize=address,undefined -shared-libsan
+  /opt/rocm/llvm/bin/clang -O1 -std=c11 -fsanitize=address,undefined -shared-libsan -fno-omit-frame-pointer \
+       -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include -I"$ROOT/include" "$ROOT/examples/batch_c.c" -o "$OUT/batch_c" \
+       -L"$OUT" -likpso -L/opt/rocm/lib -lamdhip64 -Wl,-rpath,'$ORIGIN' -Wl,-rpath,/opt/rocm/lib -Wl,-rpath,$RT -lm
+  ;;
+run)
+  export ASAN_OPTIONS=detect_leaks=0:halt_on_error=1:abort_on_error=0 UBSAN_OPTIONS=halt_on_error=1:print_stacktrace=1
+  timeout -k 10 120 "$OUT/compat_frames" 3 16384
+  timeout -k 10 120 "$OUT/batch_c" 64 100
+  timeout -k 10 120 "$OUT/compat_frames" 2 300    # ragged particle count (resident / latency paths)
+  echo ASAN_CLEAN
+  ;;
+esac
