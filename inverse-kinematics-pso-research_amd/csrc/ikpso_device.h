@@ -34,17 +34,11 @@
 // gfx950 VALU issue costs (tools/probes/valu_probe.hip, 4 waves per SIMD):
 // a wave64 v_add_u32 / v_xor_b32 / v_bitop3_b32 / v_fma_f32 on VGPR, inline or
 // literal operands issues every ~2.1-2.5 cycles per SIMD, but every
-// v_lshlrev_b32 and every VALU op that reads an SGPR takes ~4.1.  So t << 1 is
-// issued as t + t, and the sincos sign mask and the FAST-mode PSO coefficients
-// are held in VGPRs.
+// v_lshlrev_b32 and every VALU op that reads an SGPR takes ~4.1.  So the
+// generator's t << 1 is issued as t + t.  (Holding the sincos sign mask or the
+// PSO coefficients in VGPRs instead of SGPRs measured no better: DESIGN.md.)
 #ifndef IKPSO_ISSUE_SHL1_ADD
 #define IKPSO_ISSUE_SHL1_ADD 1
-#endif
-#ifndef IKPSO_ISSUE_SIGN_VGPR
-#define IKPSO_ISSUE_SIGN_VGPR 0
-#endif
-#ifndef IKPSO_ISSUE_COEF_VGPR
-#define IKPSO_ISSUE_COEF_VGPR 0
 #endif
 
 namespace ikpso {
@@ -75,27 +69,11 @@ __host__ __device__ __forceinline__ uint32_t shl1(uint32_t t)
 #endif
 }
 
-// A wave-uniform 32-bit value copied into a VGPR, so that the VALU ops reading
-// it do not take the SGPR-operand issue cost.
-__device__ __forceinline__ uint32_t to_vgpr(uint32_t s)
-{
-    uint32_t r;
-    asm("v_mov_b32 %0, %1" : "=v"(r) : "s"(s));
-    return r;
-}
-__device__ __forceinline__ float to_vgpr(float s) { return __uint_as_float(to_vgpr(__float_as_uint(s))); }
-
 // a ^ (b & 0x80000000): flip the sign of the float bits a where b's top bit is set.
 __host__ __device__ __forceinline__ uint32_t xor_sign(uint32_t a, uint32_t b)
 {
 #if defined(__HIP_DEVICE_COMPILE__)
-#if IKPSO_ISSUE_SIGN_VGPR
-    uint32_t m;
-    asm("v_mov_b32 %0, 0x80000000" : "=v"(m));
-    return __builtin_amdgcn_bitop3_b32(a, b, m, 0x78);
-#else
     return __builtin_amdgcn_bitop3_b32(a, b, 0x80000000u, 0x78);
-#endif
 #else
     return a ^ (b & 0x80000000u);
 #endif
@@ -463,10 +441,7 @@ constexpr int kTermPosRef = 1, kTermPenalty = 2, kTermRuntime = 4, kTermUniformB
 // (spills); the draws are bit-identical either way.
 template <int TERMS>
 using RngFor = XorwowT<IKPSO_ISSUE_SHL1_ADD != 0 && !(TERMS & kTermColliders)>;
-// FAST-mode PSO coefficients in VGPRs: only the resident kernel's specialised
-// (uniform-bounds) instantiations have the registers for it.
-template <int TERMS>
-constexpr bool kCoefVgpr = IKPSO_ISSUE_COEF_VGPR != 0 && (TERMS & kTermUniformBounds) && !(TERMS & kTermColliders);
+
 
 template <class Topo, int MODE, int TERMS>
 struct FitnessAcc {
@@ -605,14 +580,10 @@ struct PsoCoef {
     float wh, c1h, c2h;  // c * 2^-33
 };
 
-template <bool kVgpr = false, class CC>
+template <class CC>
 __device__ __forceinline__ PsoCoef pso_coef(const CC& cc)
 {
-    if constexpr (kVgpr)  // FAST mode's folded coefficients feed one FMA per draw
-        return PsoCoef{cc.w, cc.c1, cc.c2, to_vgpr(cc.wq), to_vgpr(cc.c1q), to_vgpr(cc.c2q),
-                       to_vgpr(cc.wh), to_vgpr(cc.c1h), to_vgpr(cc.c2h)};
-    else
-        return PsoCoef{cc.w, cc.c1, cc.c2, cc.wq, cc.c1q, cc.c2q, cc.wh, cc.c1h, cc.c2h};
+    return PsoCoef{cc.w, cc.c1, cc.c2, cc.wq, cc.c1q, cc.c2q, cc.wh, cc.c1h, cc.c2h};
 }
 
 // simulateParticlesKernel body for one dimension (src/kernel.cu:160-169):

@@ -132,7 +132,7 @@ __global__ void __launch_bounds__(kResidentMaxThreads<Topo::J>())
     copy_gbest<J, BLOCK>(sh, s_pb, bidx);
     __syncthreads();
 
-    const PsoCoef coef = pso_coef<kCoefVgpr<TERMS>>(cc);
+    const PsoCoef coef = pso_coef(cc);
     for (int it = 0; it < io.iterations; ++it) {
         compiler_fence();
         swarm_step<Topo, MODE, TERMS, BLOCK>(cc, sh, s_pb, tid, x, v, pbf, coef, rng);
