@@ -37,9 +37,10 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", type=int, default=3, choices=[3, 4, 5],
-                    help="BASELINE config: 3 = 4096 targets per GPU (default), 4 = 65536 targets over all GPUs, "
-                         "5 = 20-joint chain, 8192 targets over all GPUs, 4096 particles, penalty")
+    ap.add_argument("--config", type=int, default=3, choices=[2, 3, 4, 5],
+                    help="BASELINE config: 2 = one swarm (latency), 3 = 4096 targets per GPU (default), "
+                         "4 = 65536 targets over all GPUs, 5 = 20-joint chain, 8192 targets over all GPUs, "
+                         "4096 particles, penalty")
     ap.add_argument("--swarms-per-gpu", type=int, default=None)
     ap.add_argument("--particles", type=int, default=None)
     ap.add_argument("--iterations", type=int, default=None)
@@ -252,8 +253,9 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic (seeded targets: reset targets + U[-0.25,0.25]^3 per effector)" if args.config != 5
-                    else "synthetic (seeded targets uniform in a radius-2..4 shell)",
+            "data": {2: "the reference scene's reset targets (src/Main.cpp:334-336)",
+                     5: "synthetic (seeded targets uniform in a radius-2..4 shell)"}.get(
+                args.config, "synthetic (seeded targets: reset targets + U[-0.25,0.25]^3 per effector)"),
             "config": {
                 "workload": f"config{args.config}: {wl.description}; {P} particles, {I} PSO iterations, "
                             f"{Bl} targets per GPU ({total} total)",
@@ -271,6 +273,9 @@ def main():
         }
         if valu:
             line["roofline"]["valu"] = valu
+        if args.config == 2:
+            line["roofline"]["note"] = ("config 2 is one swarm on 4 of 256 CUs: latency-bound (SURVEY 8(d)), "
+                                        "the chip-wide fraction is not a kernel-quality figure")
         print(json.dumps(line), flush=True)
     solver.close()
     if world > 1:

@@ -213,7 +213,9 @@ ikpso_status ikpso_solver_evaluate(ikpso_solver* solver, const float* angles, co
 /* Introspection. */
 int ikpso_solver_dof(const ikpso_solver* solver);
 int ikpso_solver_effectors(const ikpso_solver* solver);
-/* Name of the kernel variant the solver dispatches to (family / topology). */
+/* Name of the kernel variant the solver dispatches to (family / topology); after a
+ * solve_batch that AUTO routed to the cooperative latency variant (a few swarms),
+ * that variant's name until the next solve. */
 const char* ikpso_solver_kernel_name(const ikpso_solver* solver);
 
 int ikpso_abi_version(void);

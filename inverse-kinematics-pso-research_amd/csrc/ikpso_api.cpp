@@ -373,6 +373,8 @@ struct ikpso_solver {
     int family = IKPSO_KERNEL_RESIDENT;
     int requested = IKPSO_KERNEL_AUTO;
     std::string kname;     // kernel family / topology, for ikpso_solver_kernel_name
+    std::string kname_latency;  // the cooperative latency variant AUTO may pick per call
+    bool last_latency = false;  // the last solve_batch ran the latency variant
     void* ws = nullptr;    // streaming / cooperative workspace
     size_t ws_bytes = 0;
     int P = 0;
@@ -581,6 +583,7 @@ ikpso_status ikpso_solver_create(const ikpso_solver_desc* desc, ikpso_solver** o
     s->family = pick_kernel(s->chain, s->mode, s->P, desc->kernel);
     s->requested = desc->kernel;
     if (s->family >= 0) s->kname = kernel_name(s->chain, s->family);
+    if (s->family >= 0) s->kname_latency = kernel_name(s->chain, IKPSO_KERNEL_COOP) + " (latency variant)";
     if (s->family < 0 || desc->kernel < IKPSO_KERNEL_AUTO || desc->kernel > IKPSO_KERNEL_COOP) {
         (void)hipFree(s->aux);
         delete s;
@@ -629,6 +632,7 @@ ikpso_status ikpso_solve_batch(ikpso_solver* s, const float* targets, const floa
     const hipStream_t hs = (hipStream_t)stream;
     const bool latency_coop = s->family == IKPSO_KERNEL_RESIDENT && s->requested == IKPSO_KERNEL_AUTO &&
                               prefer_latency_coop(s->chain, s->mode, s->P, num_swarms);
+    s->last_latency = latency_coop;
     if (s->family == IKPSO_KERNEL_RESIDENT && !latency_coop) {
         SwarmIO io{};
         io.targets = targets;
@@ -703,7 +707,7 @@ int ikpso_solver_dof(const ikpso_solver* s) { return s ? 3 * s->chain.J : 0; }
 int ikpso_solver_effectors(const ikpso_solver* s) { return s ? s->chain.E : 0; }
 const char* ikpso_solver_kernel_name(const ikpso_solver* s)
 {
-    return s ? s->kname.c_str() : "";
+    return s ? (s->last_latency ? s->kname_latency : s->kname).c_str() : "";
 }
 
 }  // extern "C"

@@ -203,8 +203,12 @@ class BatchSolver:
         self._h = handle
         self.dof = self._lib.ikpso_solver_dof(self._h)
         self.effectors = self._lib.ikpso_solver_effectors(self._h)
-        self.kernel = self._lib.ikpso_solver_kernel_name(self._h).decode()
         self.capacity = 0
+
+    @property
+    def kernel(self) -> str:
+        """Kernel variant the solver dispatches to (the last solve's, once one ran)."""
+        return self._lib.ikpso_solver_kernel_name(self._h).decode()
 
     def seed(self, capacity: int, seed_base: int = 0, first_swarm: int = 0, stream=None) -> None:
         _abi.check(self._lib.ikpso_solver_seed(self._h, int(capacity), int(seed_base), int(first_swarm),
