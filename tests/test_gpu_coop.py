@@ -79,3 +79,17 @@ def test_coop_visualiser_swarm_auto(oracle, device, monkeypatch):
     s = ikpso.BatchSolver(chain, 16384)
     assert "coop" in s.kernel
     s.close()
+
+
+def test_auto_reports_latency_variant(device):
+    """AUTO routes a few swarms to the cooperative latency variant and a full
+    batch to the resident kernel; the solver's kernel name follows each call."""
+    wl = ikpso.workload(3)
+    s = ikpso.BatchSolver(wl.chain, 1024, pso=ikpso.PSOConfig(0.5, 0.5, 1.25, 5))
+    assert s.kernel == "swarm_resident<ref_tree7>"
+    s.seed(512)
+    s.solve(dev(wl.targets(0, 1)), iterations=5)
+    assert s.kernel == "swarm_coop<ref_tree7> (latency variant)"
+    s.solve(dev(wl.targets(0, 512)), iterations=5)
+    assert s.kernel == "swarm_resident<ref_tree7>"
+    s.close()
