@@ -17,6 +17,8 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 from pathlib import Path
@@ -48,10 +50,43 @@ def parse():
     ap.add_argument("--kernel", choices=["auto", "resident", "coop", "streaming"], default="auto",
                     help="kernel family (auto: resident if the swarm fits one workgroup, else cooperative)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU baseline sample (0 = skip)")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="CPU baseline threads (0 = every CPU in this process's affinity mask)")
     ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
                     help="gloo: rehearse the N>1 path with ranks sharing the visible GPUs (not a measurement)")
     return ap.parse_args()
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(args) -> None:
+    """`--gpus N` from a plain `python bench.py`: start the N ranks as child
+    processes (one per GPU) and exit with their status.  Nothing here touches
+    the GPU, so the children start on a clean device; under torchrun
+    (WORLD_SIZE set) the world must be the one --gpus names."""
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is not None:
+        if int(world_env) != args.gpus:
+            sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world_env}")
+        return
+    if args.gpus <= 1:
+        return
+    import torch  # device_count() does not initialise the GPU on this image
+
+    ndev = torch.cuda.device_count()
+    if args.dist_backend == "nccl" and ndev < args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} needs {args.gpus} visible GPUs, found {ndev} "
+                 f"(--dist-backend gloo rehearses the N-rank path with ranks sharing the GPUs)")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", str(Path(__file__).resolve())]
+    cmd += sys.argv[1:]
+    sys.exit(subprocess.call(cmd))
 
 
 def valu_per_update(kernel: str):
@@ -68,32 +103,9 @@ def valu_per_update(kernel: str):
     return db.get(kernel)
 
 
-def cpu_baseline(wl, seconds: float, threads: int):
-    """The CPU oracle (reference algorithm restated in C, reference 4x4 FK
-    order) on a bounded sample of the same workload: batches of `threads`
-    swarms (1024 particles, 500 iterations, the same targets and seeds) until
-    `seconds` of wall time have elapsed."""
-    sys.path.insert(0, str(ROOT / "oracle"))
-    import oracle
-
-    oracle.load()
-    P, I = wl.particles, wl.iterations
-    done, t0, first = 0, time.perf_counter(), 0
-    while True:
-        B = threads
-        tg = wl.targets(first, B)
-        rng = oracle.init_generators(B * P, first * P)
-        oracle.solve_batch(wl.chain, tg, None, P, I, rng, threads=threads)
-        done += B
-        first += B
-        el = time.perf_counter() - t0
-        if el >= seconds or done >= 64 * threads:
-            break
-    ups = done * P * I / el
-    # one thread, one swarm of the same workload (SURVEY 8(d): 1 thread and all cores)
-    t1 = time.perf_counter()
-    oracle.solve_batch(wl.chain, wl.targets(first, 1), None, P, I, oracle.init_generators(P, first * P), threads=1)
-    ups1 = P * I / (time.perf_counter() - t1)
+def _cpu_facts():
+    """Host CPU model, CPUs in the machine, CPUs this process may run on, and
+    the cgroup CPU quota (CPUs' worth of time, None if unlimited)."""
     model = None
     try:
         for line in open("/proc/cpuinfo"):
@@ -102,14 +114,69 @@ def cpu_baseline(wl, seconds: float, threads: int):
                 break
     except OSError:
         pass
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        quota = None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
+    return {"cpu_model": model, "host_cpus": os.cpu_count(), "affinity_cpus": len(os.sched_getaffinity(0)),
+            "cgroup_cpu_quota": quota}
+
+
+def _cpu_sample(oracle, lib, wl, P, I, first, threads, seconds, max_batches, kw):
+    """Batches of `threads` swarms of the workload (same targets and global
+    seeds as the GPU run) until `seconds` have elapsed; returns (swarms, s)."""
+    done, t0 = 0, time.perf_counter()
+    for _ in range(max_batches):
+        tg = wl.targets(first + done, threads)
+        rng = oracle.init_generators(threads * P, (first + done) * P)
+        oracle.solve_batch(wl.chain, tg, None, P, I, rng, threads=threads, lib=lib, **kw)
+        done += threads
+        if time.perf_counter() - t0 >= seconds:
+            break
+    return done, time.perf_counter() - t0
+
+
+def cpu_baseline(seconds: float, threads: int):
+    """The CPU oracle (the reference algorithm restated in C, reference 4x4 FK
+    order, -ffp-contract=off) built -O3 -march=native on this host, OpenMP over
+    swarms, on bounded samples of configs 3 and 5 (BASELINE.md
+    §4): every CPU of the affinity mask, and one thread."""
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import oracle
+    import ikpso
+
+    facts = _cpu_facts()
+    threads = threads or facts["affinity_cpus"]
+    build = "-O3 -march=native -ffp-contract=off -fopenmp"
+    try:
+        lib = oracle.load_native()
+    except Exception as e:  # no compiler on this host: the prebuilt -O2 build
+        lib, build = oracle.load(), f"-O2 -ffp-contract=off -fopenmp (native build failed: {type(e).__name__})"
+    w3 = ikpso.workload(3)
+    P, I = w3.particles, w3.iterations
+    done, el = _cpu_sample(oracle, lib, w3, P, I, 0, threads, seconds, 64, {})
+    ups = done * P * I / el
+    d1, e1 = _cpu_sample(oracle, lib, w3, P, I, done, 1, 0.0, 1, {})  # one swarm, one thread
+    # config 5: 20-joint chain, 4096 particles, penalty; a bounded number of iterations (the cost per
+    # particle-update does not depend on I)
+    w5 = ikpso.workload(5)
+    I5 = 10
+    kw5 = {"limit_weight": w5.limit_weight, "soft_lo": w5.soft_lo, "soft_hi": w5.soft_hi}
+    d5, e5 = _cpu_sample(oracle, lib, w5, w5.particles, I5, 0, threads, seconds / 2, 16, kw5)
     return {"value": ups, "unit": "particle-updates/s", "cores": threads, "kind": "port",
-            "solves_per_s": done / el, "value_1thread": ups1, "cpu_model": model, "host_cpus": os.cpu_count(),
+            "solves_per_s": done / el, "value_1thread": d1 * P * I / e1, "build": build, **facts,
             "sample": f"{done} swarms x {P} particles x {I} iterations of config 3 (same targets/seeds), "
-                      f"OpenMP over swarms, {el:.1f} s"}
+                      f"OpenMP over swarms on {threads} threads, {el:.1f} s; 1 thread: 1 swarm, {e1:.1f} s",
+            "config5": {"value": d5 * w5.particles * I5 / e5, "unit": "particle-updates/s", "cores": threads,
+                        "sample": f"{d5} swarms x {w5.particles} particles x {I5} iterations of config 5, "
+                                  f"{e5:.1f} s"}}
 
 
 def main():
     args = parse()
+    launch_ranks(args)
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -229,6 +296,15 @@ def main():
             "traffic": round(vpu["hbm_bytes_per_update"] * ups_launch) if vpu else None,
             "kernel": solver.kernel + (" (I+2 launches per batch)" if streaming else " (one launch = one batch)"),
             "kernel_ms": round(kern_ms, 3),
+            "hbm_measured": None if not vpu else {
+                "achieved": round(ups_launch * vpu["hbm_bytes_per_update"] / kern_s / 1e9, 2),
+                "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(ups_launch * vpu["hbm_bytes_per_update"] / kern_s / 1e9 / HBM_PEAK_GBS, 6),
+                "bytes_per_update": vpu["hbm_bytes_per_update"],
+                "note": "counter-measured HBM bytes per particle-update ((2*FETCH_SIZE + WRITE_SIZE) of the "
+                        "kernel's dispatch, profiles/valu_per_update.json) x the live update rate: the swarm "
+                        "state stays on chip, HBM carries only generator states, inputs and results",
+            },
             "hbm_algorithmic": {
                 "achieved": round(alg_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(alg_gbs / HBM_PEAK_GBS, 4),
@@ -238,8 +314,10 @@ def main():
             },
         }
         cpu = None
-        if world == 1 and args.cpu_seconds > 0 and args.config == 3:
-            cpu = cpu_baseline(wl, args.cpu_seconds, args.cpu_threads)
+        if world == 1 and args.cpu_seconds > 0 and args.config in (3, 5):
+            cpu = cpu_baseline(args.cpu_seconds, args.cpu_threads)
+            if args.config == 5:  # the config-5 figure is this line's baseline
+                cpu = dict(cpu, value=cpu["config5"]["value"], sample=cpu["config5"]["sample"])
         line = {
             "metric": "PSO particle-updates/sec + IK solves/sec, 7-DOF 1024-particle swarm" if args.config != 5
                       else "PSO particle-updates/sec + IK solves/sec, 20-DOF 4096-particle swarm (config 5)",

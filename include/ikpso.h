@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define IKPSO_ABI_VERSION 2
+#define IKPSO_ABI_VERSION 3
 
 typedef int ikpso_status;
 enum {
@@ -196,11 +196,23 @@ ikpso_status ikpso_solver_seed(ikpso_solver* solver, int64_t capacity, uint64_t 
  * concurrent.  The cooperative family needs its workgroups co-resident (one per
  * CU): the grid is checked against the occupancy query at launch, and if other
  * work on the device still keeps a group from assembling, its bounded wait
- * gives up and the swarms it had not finished get a NaN fitness (never a
- * hang); ikpso_calculate_pso reports this as IKPSO_ERR_HIP. */
+ * gives up (never a hang) and the swarms it had not finished get NaN angles,
+ * fitness and residual -- until ikpso_solver_sync settles the solve. */
 ikpso_status ikpso_solve_batch(ikpso_solver* solver, const float* targets, const float* start_pose,
                                int64_t num_swarms, int32_t iterations, float* out_angles, float* out_fitness,
                                float* out_residual, void* stream);
+
+/* Settle the last solve_batch (ABI >= 3).  After a cooperative-family solve:
+ * wait for it and, if a group gave up (the GPU shared with other work), restore
+ * the generator states from the snapshot taken before the launch and re-run the
+ * batch on the streaming kernels, which need no co-residency, so the outputs are
+ * always a complete solve.  Returns at once after the other families.  The
+ * buffers passed to that solve_batch must still be valid.  solve_batch settles a
+ * pending solve itself before it launches the next one. */
+ikpso_status ikpso_solver_sync(ikpso_solver* solver);
+/* Solves of this handle / of the process that took the streaming fallback. */
+int64_t ikpso_solver_fallbacks(const ikpso_solver* solver);
+int64_t ikpso_coop_fallbacks(void);
 
 /* Evaluate the device FK + fitness for n angle vectors (no PSO):
  *   angles device [n][D]; targets device [n][E][3] or NULL (chain targets);

@@ -8,6 +8,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <atomic>
 #include <mutex>
 #include <new>
 #include <vector>
@@ -26,6 +27,7 @@ static_assert(sizeof(ikpso_collider) == 48, "obj_t is 48 bytes");
 namespace {
 
 thread_local int g_last_hip_error = 0;
+std::atomic<int64_t> g_coop_fallbacks{0};  // cooperative solves re-run on the streaming kernels
 
 ikpso_status hip_status(hipError_t e)
 {
@@ -338,10 +340,19 @@ bool prefer_latency_coop(const ChainHost& ch, int mode, int P, int64_t B)
     return coop_plan(ch, mode, P, B, true, &G, &NG, &T) && T == kCoopLatencyThreads;
 }
 
+// Bound on a cooperative group wait (IKPSO_COOP_SPIN_LIMIT: debug knob; 0
+// forces the give-up path so the fallback can be tested).
+uint32_t coop_spin_limit()
+{
+    const char* e = getenv("IKPSO_COOP_SPIN_LIMIT");
+    return e ? (uint32_t)strtoul(e, nullptr, 10) : kCoopSpinLimit;
+}
+
 // Point the coop fields of `io` into workspace `ws` (coop_workspace_bytes) and
 // clear the counters and the error flag.
 hipError_t carve_coop(SwarmIO& io, void* ws, int G, int NG, int block, int D, hipStream_t s)
 {
+    io.coop_spin_limit = coop_spin_limit();
     Carver cv{static_cast<char*>(ws)};
     io.coop_counter = cv.take<uint32_t>((size_t)NG * kCoopCounterStride);
     io.coop_error = cv.take<int32_t>(1);
@@ -381,7 +392,62 @@ struct ikpso_solver {
     int mode = IKPSO_ARITH_FAST;
     ikpso_rng_state* rng = nullptr;
     int64_t capacity = 0;
+    // Cooperative solves: the generator states as they were before the launch,
+    // and what ikpso_solver_sync needs to re-run the batch on the streaming
+    // kernels if a group could not assemble.
+    ikpso_rng_state* rng_snap = nullptr;
+    int64_t snap_capacity = 0;
+    void* ws_fallback = nullptr;
+    size_t ws_fallback_bytes = 0;
+    struct {
+        bool active = false;
+        const float* targets = nullptr;
+        const float* start_pose = nullptr;
+        int64_t num_swarms = 0;
+        int32_t iterations = 0;
+        float *out_angles = nullptr, *out_fitness = nullptr, *out_residual = nullptr;
+        hipStream_t stream = nullptr;
+        const int32_t* error = nullptr;  // device flag in ws
+    } pending;
+    int64_t fallbacks = 0;
 };
+
+namespace {
+
+// Grow a device buffer to at least `need` bytes (contents not kept).
+ikpso_status grow(void** buf, size_t* have, size_t need)
+{
+    if (need <= *have) return IKPSO_OK;
+    if (*buf) IKPSO_HIP(hipFree(*buf));  // hipFree synchronises the device
+    *buf = nullptr;
+    *have = 0;
+    IKPSO_HIP(hipMalloc(buf, need));
+    *have = need;
+    return IKPSO_OK;
+}
+
+// The batch on the streaming kernels (state in HBM, I + 2 launches; no
+// co-residency requirement).
+ikpso_status solve_streaming(ikpso_solver* s, void** ws, size_t* ws_bytes, const float* targets,
+                             const float* start_pose, int64_t num_swarms, int32_t iterations, float* out_angles,
+                             float* out_fitness, float* out_residual, hipStream_t hs)
+{
+    const int D = 3 * s->chain.J;
+    ikpso_status st = grow(ws, ws_bytes, stream_workspace_bytes(num_swarms, s->P, D, true));
+    if (st != IKPSO_OK) return st;
+    StreamIO io{};
+    carve_stream(io, *ws, num_swarms, s->P, D, true);
+    io.rng_aos = s->rng;
+    io.targets = targets;
+    io.start_pose = start_pose;
+    io.out_angles = out_angles;
+    io.out_fitness = out_fitness;
+    io.out_residual = out_residual;
+    IKPSO_HIP(launch_stream(s->chain, s->mode, io, iterations, hs));
+    return IKPSO_OK;
+}
+
+}  // namespace
 
 extern "C" {
 
@@ -466,14 +532,18 @@ ikpso_status ikpso_calculate_pso(float* particles, const float* positions, float
         return IKPSO_ERR_UNSUPPORTED;
 
     std::lock_guard<std::mutex> lk(g_scratch_mu);
-    // device scratch: [result D | aux (64-float aligned) | streaming workspace];
-    // aux is uploaded here and the call synchronises before returning, so
-    // `ch.aux` outlives every use
+    // device scratch: [result D | aux (64-float aligned) | workspace]; aux is
+    // uploaded here and the call synchronises before returning, so `ch.aux`
+    // outlives every use.  The cooperative path also keeps a snapshot of the
+    // generator states and room for the streaming fallback.
     const size_t aux_at = ((size_t)D + 63) & ~size_t(63);
     const size_t head = sizeof(float) * (aux_at + ch.aux.size());
-    const size_t ws = family_run == IKPSO_KERNEL_STREAMING ? stream_workspace_bytes(1, size, D, false)
-                      : family_run == IKPSO_KERNEL_COOP    ? coop_workspace_bytes(cng, cg, D)
-                                                           : 0;
+    const size_t sws = stream_workspace_bytes(1, size, D, false);
+    const size_t snap = ((sizeof(ikpso_rng_state) * (size_t)size + 255) & ~size_t(255));
+    const size_t ws = family_run == IKPSO_KERNEL_STREAMING ? sws
+                      : family_run == IKPSO_KERNEL_COOP
+                          ? ((coop_workspace_bytes(cng, cg, D) + 255) & ~size_t(255)) + snap + sws
+                          : 0;
     float* dres = nullptr;
     st = scratch(((head + 255) & ~size_t(255)) + ws, &dres);
     if (st != IKPSO_OK) return st;
@@ -499,14 +569,30 @@ ikpso_status ikpso_calculate_pso(float* particles, const float* positions, float
         io.P = size;
         io.iterations = pso.iterations;
         io.num_swarms = 1;
-        IKPSO_HIP(carve_coop(io, reinterpret_cast<char*>(dres) + ((head + 255) & ~size_t(255)), cg, cng, cblk, D, s));
+        char* wsb = reinterpret_cast<char*>(dres) + ((head + 255) & ~size_t(255));
+        ikpso_rng_state* rsnap =
+            reinterpret_cast<ikpso_rng_state*>(wsb + ((coop_workspace_bytes(cng, cg, D) + 255) & ~size_t(255)));
+        IKPSO_HIP(hipMemcpyAsync(rsnap, randoms, sizeof(ikpso_rng_state) * (size_t)size, hipMemcpyDeviceToDevice, s));
+        IKPSO_HIP(carve_coop(io, wsb, cg, cng, cblk, D, s));
         IKPSO_HIP(launch_coop(ch, mode, io, s));
         int32_t err = 0;
-        IKPSO_HIP(hipMemcpyAsync(result, dres, sizeof(float) * D, hipMemcpyDefault, s));
         IKPSO_HIP(hipMemcpyAsync(&err, io.coop_error, sizeof(err), hipMemcpyDeviceToHost, s));
         IKPSO_HIP(hipStreamSynchronize(s));
-        if (err) return hip_status(hipErrorLaunchTimeOut);
-        return IKPSO_OK;
+        if (err) {
+            // The group could not assemble (other work held CUs): restore the
+            // generator states and solve on the streaming kernels, which need
+            // no co-residency -- the caller never sees the contention.
+            IKPSO_HIP(hipMemcpyAsync(randoms, rsnap, sizeof(ikpso_rng_state) * (size_t)size, hipMemcpyDeviceToDevice,
+                                     s));
+            StreamIO sio{};
+            carve_stream(sio, reinterpret_cast<char*>(rsnap) + snap, 1, size, D, false);
+            sio.state = particles;
+            sio.pbf = bests;
+            sio.rng_aos = randoms;
+            sio.out_angles = dres;
+            IKPSO_HIP(launch_stream(ch, mode, sio, pso.iterations, s));
+            g_coop_fallbacks.fetch_add(1);
+        }
     } else {
         StreamIO io{};
         carve_stream(io, reinterpret_cast<char*>(dres) + ((head + 255) & ~size_t(255)), 1, size, D, false);
@@ -598,6 +684,8 @@ ikpso_status ikpso_solver_destroy(ikpso_solver* s)
 {
     if (!s) return IKPSO_OK;
     if (s->rng) (void)hipFree(s->rng);
+    if (s->rng_snap) (void)hipFree(s->rng_snap);
+    if (s->ws_fallback) (void)hipFree(s->ws_fallback);
     if (s->aux) (void)hipFree(s->aux);
     if (s->ws) (void)hipFree(s->ws);
     delete s;
@@ -630,6 +718,10 @@ ikpso_status ikpso_solve_batch(ikpso_solver* s, const float* targets, const floa
     if (num_swarms > s->capacity || !s->rng) return IKPSO_ERR_INVALID_ARG;  // seed first
     if (num_swarms > 0x7fffffff) return IKPSO_ERR_INVALID_ARG;
     const hipStream_t hs = (hipStream_t)stream;
+    if (s->pending.active) {  // the previous cooperative solve was not synced: settle it first
+        const ikpso_status st = ikpso_solver_sync(s);
+        if (st != IKPSO_OK) return st;
+    }
     const bool latency_coop = s->family == IKPSO_KERNEL_RESIDENT && s->requested == IKPSO_KERNEL_AUTO &&
                               prefer_latency_coop(s->chain, s->mode, s->P, num_swarms);
     s->last_latency = latency_coop;
@@ -652,14 +744,19 @@ ikpso_status ikpso_solve_batch(ikpso_solver* s, const float* targets, const floa
         int G, NG, T;
         if (!coop_plan(s->chain, s->mode, s->P, num_swarms, s->requested == IKPSO_KERNEL_AUTO, &G, &NG, &T))
             return IKPSO_ERR_UNSUPPORTED;
-        const size_t need = coop_workspace_bytes(NG, G, D);
-        if (need > s->ws_bytes) {
-            if (s->ws) IKPSO_HIP(hipFree(s->ws));
-            s->ws = nullptr;
-            s->ws_bytes = 0;
-            IKPSO_HIP(hipMalloc(&s->ws, need));
-            s->ws_bytes = need;
+        ikpso_status st = grow(&s->ws, &s->ws_bytes, coop_workspace_bytes(NG, G, D));
+        if (st != IKPSO_OK) return st;
+        // snapshot of the generator states the launch starts from (48 B per
+        // particle, one D2D copy): the fallback re-runs the batch from it
+        if (num_swarms > s->snap_capacity) {
+            if (s->rng_snap) IKPSO_HIP(hipFree(s->rng_snap));
+            s->rng_snap = nullptr;
+            s->snap_capacity = 0;
+            IKPSO_HIP(hipMalloc(&s->rng_snap, sizeof(ikpso_rng_state) * (size_t)s->capacity * s->P));
+            s->snap_capacity = s->capacity;
         }
+        IKPSO_HIP(hipMemcpyAsync(s->rng_snap, s->rng, sizeof(ikpso_rng_state) * (size_t)num_swarms * s->P,
+                                 hipMemcpyDeviceToDevice, hs));
         SwarmIO io{};
         io.targets = targets;
         io.start_pose = start_pose;
@@ -672,27 +769,49 @@ ikpso_status ikpso_solve_batch(ikpso_solver* s, const float* targets, const floa
         io.num_swarms = num_swarms;
         IKPSO_HIP(carve_coop(io, s->ws, G, NG, T, D, hs));
         IKPSO_HIP(launch_coop(s->chain, s->mode, io, hs));
+        s->pending.active = true;
+        s->pending.targets = targets;
+        s->pending.start_pose = start_pose;
+        s->pending.num_swarms = num_swarms;
+        s->pending.iterations = iterations;
+        s->pending.out_angles = out_angles;
+        s->pending.out_fitness = out_fitness;
+        s->pending.out_residual = out_residual;
+        s->pending.stream = hs;
+        s->pending.error = io.coop_error;
         return IKPSO_OK;
     }
-    const size_t need = stream_workspace_bytes(num_swarms, s->P, D, true);
-    if (need > s->ws_bytes) {
-        if (s->ws) IKPSO_HIP(hipFree(s->ws));  // hipFree synchronises the device
-        s->ws = nullptr;
-        s->ws_bytes = 0;
-        IKPSO_HIP(hipMalloc(&s->ws, need));
-        s->ws_bytes = need;
-    }
-    StreamIO io{};
-    carve_stream(io, s->ws, num_swarms, s->P, D, true);
-    io.rng_aos = s->rng;
-    io.targets = targets;
-    io.start_pose = start_pose;
-    io.out_angles = out_angles;
-    io.out_fitness = out_fitness;
-    io.out_residual = out_residual;
-    IKPSO_HIP(launch_stream(s->chain, s->mode, io, iterations, hs));
+    return solve_streaming(s, &s->ws, &s->ws_bytes, targets, start_pose, num_swarms, iterations, out_angles,
+                           out_fitness, out_residual, hs);
+}
+
+ikpso_status ikpso_solver_sync(ikpso_solver* s)
+{
+    if (!s) return IKPSO_ERR_INVALID_ARG;
+    if (!s->pending.active) return IKPSO_OK;
+    auto& p = s->pending;
+    p.active = false;
+    int32_t err = 0;
+    IKPSO_HIP(hipMemcpyAsync(&err, p.error, sizeof(err), hipMemcpyDeviceToHost, p.stream));
+    IKPSO_HIP(hipStreamSynchronize(p.stream));
+    if (!err) return IKPSO_OK;
+    // A group gave up waiting for its members (the GPU is shared): restore the
+    // generator states and solve the whole batch on the streaming kernels.
+    IKPSO_HIP(hipMemcpyAsync(s->rng, s->rng_snap, sizeof(ikpso_rng_state) * (size_t)p.num_swarms * s->P,
+                             hipMemcpyDeviceToDevice, p.stream));
+    const ikpso_status st = solve_streaming(s, &s->ws_fallback, &s->ws_fallback_bytes, p.targets, p.start_pose,
+                                            p.num_swarms, p.iterations, p.out_angles, p.out_fitness, p.out_residual,
+                                            p.stream);
+    if (st != IKPSO_OK) return st;
+    IKPSO_HIP(hipStreamSynchronize(p.stream));
+    ++s->fallbacks;
+    g_coop_fallbacks.fetch_add(1);
     return IKPSO_OK;
 }
+
+int64_t ikpso_solver_fallbacks(const ikpso_solver* s) { return s ? s->fallbacks : 0; }
+
+int64_t ikpso_coop_fallbacks(void) { return g_coop_fallbacks.load(); }
 
 ikpso_status ikpso_solver_evaluate(ikpso_solver* s, const float* angles, const float* targets, const float* rest,
                                    int64_t n, float* out_fitness, float* out_positions, void* stream)

@@ -38,7 +38,6 @@
 
 namespace ikpso {
 
-constexpr uint32_t kCoopSpinLimit = 1u << 22;
 
 __device__ __forceinline__ void st_sc1(float* p, float v)
 {
@@ -75,7 +74,7 @@ struct CoopShared {
 // always when `force`).  Called by every wave; wave 0 does the global work.
 template <int J, int BLOCK>
 __device__ __forceinline__ void coop_exchange(SwarmShared<J>& sh, CoopShared<J>& cs, const float* s_pb,
-                                              uint32_t local_key, int32_t* error, bool force)
+                                              uint32_t local_key, int32_t* error, uint32_t spin_limit, bool force)
 {
     constexpr int D = 3 * J;
     constexpr int SLOT = kCoopSlot(D);
@@ -102,11 +101,11 @@ __device__ __forceinline__ void coop_exchange(SwarmShared<J>& sh, CoopShared<J>&
             __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             uint32_t n = 0;
             while (ld_sc1(counter) < target) {
-                __builtin_amdgcn_s_sleep(2);
-                if (++n > kCoopSpinLimit) {
+                if (n++ >= spin_limit) {
                     timed_out = 1;
                     break;
                 }
+                __builtin_amdgcn_s_sleep(2);
             }
         }
         timed_out = __builtin_amdgcn_readfirstlane(timed_out);  // lane 0's verdict
@@ -188,14 +187,14 @@ __global__ void __launch_bounds__(BLOCK, (BLOCK >= 256 ? BLOCK / 256 : 1))
         }
         float pbf = fitness<Topo, MODE, TERMS>(cc, x, sh.rest, sh.tgt, nullptr);
         // swarm argmin + unconditional first global-best copy (src/kernel.cu:297-304)
-        coop_exchange<J, BLOCK>(sh, cs, s_pb, i < P ? ordered_key(pbf) : 0xFFFFFFFFu, io.coop_error, true);
+        coop_exchange<J, BLOCK>(sh, cs, s_pb, i < P ? ordered_key(pbf) : 0xFFFFFFFFu, io.coop_error, io.coop_spin_limit, true);
 
         for (int it = 0; it < io.iterations; ++it) {
             compiler_fence();
             if (cs.abort) break;
             swarm_step<Topo, MODE, TERMS, BLOCK>(cc, sh, s_pb, tid, x, v, pbf, coef, rng);
             const bool act = cs.member * BLOCK + tid < P;
-            coop_exchange<J, BLOCK>(sh, cs, s_pb, act ? ordered_key(pbf) : 0xFFFFFFFFu, io.coop_error, false);
+            coop_exchange<J, BLOCK>(sh, cs, s_pb, act ? ordered_key(pbf) : 0xFFFFFFFFu, io.coop_error, io.coop_spin_limit, false);
         }
 
         compiler_fence();
@@ -228,8 +227,12 @@ __global__ void __launch_bounds__(BLOCK, (BLOCK >= 256 ? BLOCK / 256 : 1))
         }
         __syncthreads();  // sh / s_pb are reused by the next swarm; every wave has read cs
         if (cs.abort) {     // a wait timed out: mark this and every later swarm of the group as failed
-            for (int64_t r = bb; r < io.num_swarms; r += io.coop_ng)
-                if (member == 0 && tid == 0 && io.out_fitness) io.out_fitness[r] = __builtin_nanf("");
+            if (member == 0)
+                for (int64_t r = bb; r < io.num_swarms; r += io.coop_ng) {
+                    if (tid < D) io.out_angles[r * D + tid] = __builtin_nanf("");
+                    if (tid == 0 && io.out_fitness) io.out_fitness[r] = __builtin_nanf("");
+                    if (tid == 0 && io.out_residual) io.out_residual[r] = __builtin_nanf("");
+                }
             break;
         }
         if (tid == 0) cs.b = bb + io.coop_ng;

@@ -85,6 +85,10 @@ __host__ __device__ constexpr int kCoopThreads()
 __host__ __device__ constexpr int kCoopSlot(int D) { return ((D + 2 + 15) / 16) * 16; }
 
 constexpr int kCoopCounterStride = 32;
+// Default bound on a cooperative group wait (polls of ~1 us each): seconds,
+// against ~2 us per exchange when the group is co-resident.
+// IKPSO_COOP_SPIN_LIMIT overrides it (0 forces the give-up path: fallback tests).
+constexpr uint32_t kCoopSpinLimit = 1u << 22;
 // Latency variant of the cooperative kernel (few swarms): 256-lane chunks,
 // one wave per SIMD, a swarm of 1024 over 4 CUs.
 #ifndef IKPSO_COOP_LATENCY_THREADS

@@ -141,8 +141,9 @@ bool coop_geometry(const ChainHost& ch, int mode, CoopGeometry* g)
         }
     });
     if (!spec) return false;
-    int cus = 0;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0) != hipSuccess || cus <= 0) return false;
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return false;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) return false;
     g->blocks_per_cu = 1;
     g->cus = cus;
     return true;

@@ -57,7 +57,7 @@ struct SwarmIO {
     int32_t coop_g;
     int32_t coop_ng;
     int32_t coop_block;       // workgroup size (kCoopThreads<J>() or kCoopLatencyThreads)
-    int32_t pad_;
+    uint32_t coop_spin_limit; // polls before a group wait gives up (0: give up at the first unmet poll)
 };
 
 // Streaming (state-in-HBM) kernels: one launch per PSO iteration over every

@@ -72,7 +72,7 @@ COLLIDER_DTYPE = np.dtype(
 )
 assert COLLIDER_DTYPE.itemsize == 48
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 FLAG_POSREF_NODE_SLOT = 1  # IKPSO_FLAG_POSREF_NODE_SLOT
 
@@ -135,6 +135,9 @@ SIGNATURES = {
     "ikpso_solver_destroy": (_i32, [_vp]),
     "ikpso_solver_seed": (_i32, [_vp, _i64, _u64, _i64, _vp]),
     "ikpso_solve_batch": (_i32, [_vp, _vp, _vp, _i64, _i32, _vp, _vp, _vp, _vp]),
+    "ikpso_solver_sync": (_i32, [_vp]),
+    "ikpso_solver_fallbacks": (_i64, [_vp]),
+    "ikpso_coop_fallbacks": (_i64, []),
     "ikpso_solver_evaluate": (_i32, [_vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp]),
     "ikpso_solver_dof": (ctypes.c_int, [_vp]),
     "ikpso_solver_effectors": (ctypes.c_int, [_vp]),

@@ -211,14 +211,32 @@ class BatchSolver:
         return self._lib.ikpso_solver_kernel_name(self._h).decode()
 
     def seed(self, capacity: int, seed_base: int = 0, first_swarm: int = 0, stream=None) -> None:
+        torch = _torch()
         _abi.check(self._lib.ikpso_solver_seed(self._h, int(capacity), int(seed_base), int(first_swarm),
                                                _stream_handle(stream)), "ikpso_solver_seed")
+        self._device = torch.device("cuda", torch.cuda.current_device())  # where the generator states live
         self.capacity = max(self.capacity, int(capacity))
 
+    def _check_tensor(self, t, name: str, device) -> None:
+        """float32, contiguous, on the solver's device (the kernels read raw fp32)."""
+        torch = _torch()
+        if t is None:
+            return
+        if not t.is_cuda or t.device != device:
+            raise ValueError(f"{name} must be on {device}, got {t.device}")
+        if t.dtype != torch.float32:
+            raise ValueError(f"{name} must be float32, got {t.dtype}")
+        if not t.is_contiguous():
+            raise ValueError(f"{name} must be contiguous")
+
     def solve(self, targets=None, start_pose=None, iterations: Optional[int] = None, num_swarms: Optional[int] = None,
-              out: Optional[Tuple] = None, residual: bool = True, stream=None):
+              out: Optional[Tuple] = None, residual: bool = True, stream=None, sync: bool = True):
         """targets: device [B, E, 3] (None: chain targets); start_pose: device [B, D] or None.
-        Returns (angles [B, D], fitness [B], residual [B] or None) device tensors."""
+        Returns (angles [B, D], fitness [B], residual [B] or None) device tensors.
+        sync: settle a cooperative-family solve before returning (ikpso_solver_sync:
+        waits for it, and re-runs it on the streaming kernels if the GPU's other work
+        kept a group from assembling); no effect on the other families, which stay
+        stream-ordered and asynchronous."""
         torch = _torch()
         if num_swarms is None:
             if targets is None:
@@ -230,22 +248,43 @@ class BatchSolver:
             raise ValueError(f"targets must be [{B}, {self.effectors}, 3]")
         if start_pose is not None and tuple(start_pose.shape) != (B, self.dof):
             raise ValueError(f"start_pose must be [{B}, {self.dof}]")
-        dev = targets.device if targets is not None else torch.device("cuda")
+        dev = getattr(self, "_device", None) or torch.device("cuda", torch.cuda.current_device())
         if out is None:
             angles = torch.empty((B, self.dof), dtype=torch.float32, device=dev)
             fitness = torch.empty((B,), dtype=torch.float32, device=dev)
             res = torch.empty((B,), dtype=torch.float32, device=dev) if residual else None
         else:
             angles, fitness, res = out
+            if tuple(angles.shape) != (B, self.dof) or tuple(fitness.shape) != (B,) or (
+                    res is not None and tuple(res.shape) != (B,)):
+                raise ValueError("out must be ([B, D], [B], [B] or None)")
+        for t, name in ((targets, "targets"), (start_pose, "start_pose"), (angles, "out angles"),
+                        (fitness, "out fitness"), (res, "out residual")):
+            self._check_tensor(t, name, dev)
         _abi.check(self._lib.ikpso_solve_batch(self._h, _dev_ptr(targets), _dev_ptr(start_pose), B, it,
                                                _dev_ptr(angles), _dev_ptr(fitness), _dev_ptr(res),
                                                _stream_handle(stream)), "ikpso_solve_batch")
+        if sync:
+            _abi.check(self._lib.ikpso_solver_sync(self._h), "ikpso_solver_sync")
         return angles, fitness, res
+
+    def sync(self) -> None:
+        """ikpso_solver_sync: settle the last solve (see solve(sync=...))."""
+        _abi.check(self._lib.ikpso_solver_sync(self._h), "ikpso_solver_sync")
+
+    @property
+    def fallbacks(self) -> int:
+        """Cooperative solves of this solver that were re-run on the streaming kernels."""
+        return int(self._lib.ikpso_solver_fallbacks(self._h))
 
     def evaluate(self, angles, targets=None, rest=None, stream=None):
         """Device FK + fitness for angle vectors [n, D]: (fitness [n], node positions [n, J, 3])."""
         torch = _torch()
         n = int(angles.shape[0])
+        if tuple(angles.shape) != (n, self.dof):
+            raise ValueError(f"angles must be [n, {self.dof}]")
+        for t, name in ((angles, "angles"), (targets, "targets"), (rest, "rest")):
+            self._check_tensor(t, name, angles.device)
         fit = torch.empty((n,), dtype=torch.float32, device=angles.device)
         pos = torch.empty((n, self.dof // 3, 3), dtype=torch.float32, device=angles.device)
         _abi.check(self._lib.ikpso_solver_evaluate(self._h, _dev_ptr(angles), _dev_ptr(targets), _dev_ptr(rest), n,

@@ -38,7 +38,9 @@ BOX_DTYPE = np.dtype(
 )
 
 _LIB = None
+_NATIVE = None
 _P = ctypes.c_void_p
+NATIVE_PATH = HERE / "_build" / "native" / "libikpso_oracle.so"
 
 
 def build() -> Path:
@@ -51,48 +53,61 @@ def load():
     if _LIB is None:
         if not LIB_PATH.exists():
             build()
-        lib = ctypes.CDLL(str(LIB_PATH))
-        sig = {
-            "orc_sizeof_rng": (ctypes.c_int, []),
-            "orc_sizeof_node": (ctypes.c_int, []),
-            "orc_curand_init": (None, [ctypes.c_uint64, _P]),
-            "orc_curand": (ctypes.c_uint32, [_P]),
-            "orc_curand_uniform": (ctypes.c_float, [_P]),
-            "orc_init_generators": (None, [_P, ctypes.c_int64, ctypes.c_uint64]),
-            "orc_uniform_stream": (None, [_P, _P, ctypes.c_int]),
-            "orc_chain_matrices": (None, [_P, ctypes.c_int, _P, _P]),
-            "orc_fitness": (ctypes.c_float, [_P, ctypes.c_int, _P, _P, ctypes.c_float, ctypes.c_float]),
-            "orc_fitness_ex": (ctypes.c_float, [_P, ctypes.c_int, _P, _P, ctypes.c_float, ctypes.c_float,
-                                                ctypes.c_float, _P, _P, _P, ctypes.c_int]),
-            "orc_sizeof_box": (ctypes.c_int, []),
-            "orc_gjk_intersect": (ctypes.c_int, [_P, _P]),
-            "orc_node_collides": (ctypes.c_int, [_P, _P, ctypes.c_float, _P, ctypes.c_int]),
-            "orc_node_positions": (None, [_P, ctypes.c_int, _P, _P]),
-            "orc_residual": (ctypes.c_float, [_P, ctypes.c_int, _P]),
-            "orc_calculate_pso": (
-                ctypes.c_int,
-                [_P, _P, _P, _P, ctypes.c_int64, _P, ctypes.c_int, ctypes.c_float, ctypes.c_float, ctypes.c_float,
-                 ctypes.c_int, ctypes.c_float, ctypes.c_float, _P],
-            ),
-            "orc_calculate_pso_ex": (
-                ctypes.c_int,
-                [_P, _P, _P, _P, ctypes.c_int64, _P, ctypes.c_int, ctypes.c_float, ctypes.c_float, ctypes.c_float,
-                 ctypes.c_int, ctypes.c_float, ctypes.c_float, _P, ctypes.c_float, _P, _P, _P, ctypes.c_int],
-            ),
-            "orc_solve_batch": (
-                ctypes.c_int,
-                [_P, ctypes.c_int, _P, _P, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_float,
-                 ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float, _P, _P, _P, _P, _P, ctypes.c_int,
-                 ctypes.c_float, _P, _P, _P, ctypes.c_int],
-            ),
-        }
-        for name, (res, args) in sig.items():
-            fn = getattr(lib, name)
-            fn.restype = res
-            fn.argtypes = args
-        assert lib.orc_sizeof_rng() == 48 and lib.orc_sizeof_node() == 88 and lib.orc_sizeof_box() == 48
-        _LIB = lib
+        _LIB = _bind(ctypes.CDLL(str(LIB_PATH)))
     return _LIB
+
+
+def load_native():
+    """The CPU-baseline build of the same source (-O3 -march=native, still
+    -ffp-contract=off: same results), compiled for the host this runs on."""
+    global _NATIVE
+    if _NATIVE is None:
+        subprocess.run(["make", "-s", "-C", str(HERE), "native"], check=True)
+        _NATIVE = _bind(ctypes.CDLL(str(NATIVE_PATH)))
+    return _NATIVE
+
+
+def _bind(lib):
+    sig = {
+        "orc_sizeof_rng": (ctypes.c_int, []),
+        "orc_sizeof_node": (ctypes.c_int, []),
+        "orc_curand_init": (None, [ctypes.c_uint64, _P]),
+        "orc_curand": (ctypes.c_uint32, [_P]),
+        "orc_curand_uniform": (ctypes.c_float, [_P]),
+        "orc_init_generators": (None, [_P, ctypes.c_int64, ctypes.c_uint64]),
+        "orc_uniform_stream": (None, [_P, _P, ctypes.c_int]),
+        "orc_chain_matrices": (None, [_P, ctypes.c_int, _P, _P]),
+        "orc_fitness": (ctypes.c_float, [_P, ctypes.c_int, _P, _P, ctypes.c_float, ctypes.c_float]),
+        "orc_fitness_ex": (ctypes.c_float, [_P, ctypes.c_int, _P, _P, ctypes.c_float, ctypes.c_float,
+                                            ctypes.c_float, _P, _P, _P, ctypes.c_int]),
+        "orc_sizeof_box": (ctypes.c_int, []),
+        "orc_gjk_intersect": (ctypes.c_int, [_P, _P]),
+        "orc_node_collides": (ctypes.c_int, [_P, _P, ctypes.c_float, _P, ctypes.c_int]),
+        "orc_node_positions": (None, [_P, ctypes.c_int, _P, _P]),
+        "orc_residual": (ctypes.c_float, [_P, ctypes.c_int, _P]),
+        "orc_calculate_pso": (
+            ctypes.c_int,
+            [_P, _P, _P, _P, ctypes.c_int64, _P, ctypes.c_int, ctypes.c_float, ctypes.c_float, ctypes.c_float,
+             ctypes.c_int, ctypes.c_float, ctypes.c_float, _P],
+        ),
+        "orc_calculate_pso_ex": (
+            ctypes.c_int,
+            [_P, _P, _P, _P, ctypes.c_int64, _P, ctypes.c_int, ctypes.c_float, ctypes.c_float, ctypes.c_float,
+             ctypes.c_int, ctypes.c_float, ctypes.c_float, _P, ctypes.c_float, _P, _P, _P, ctypes.c_int],
+        ),
+        "orc_solve_batch": (
+            ctypes.c_int,
+            [_P, ctypes.c_int, _P, _P, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_float,
+             ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float, _P, _P, _P, _P, _P, ctypes.c_int,
+             ctypes.c_float, _P, _P, _P, ctypes.c_int],
+        ),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    assert lib.orc_sizeof_rng() == 48 and lib.orc_sizeof_node() == 88 and lib.orc_sizeof_box() == 48
+    return lib
 
 
 def _p(a):
@@ -204,8 +219,9 @@ def calculate_pso(chain, size: int, randoms: np.ndarray, inertia=0.5, local=0.5,
 
 def solve_batch(chain, targets, start_pose, particles: int, iterations: int, rng: np.ndarray, inertia=0.5,
                 local=0.5, glob=1.25, angle_weight=3.0, distance_weight=0.0, positions=None, threads: int = 0,
-                limit_weight=0.0, soft_lo=None, soft_hi=None, colliders=None):
+                limit_weight=0.0, soft_lo=None, soft_hi=None, colliders=None, lib=None):
     """B independent reference solves (OpenMP over swarms).  rng: [B*P] states, advanced in place.
+    lib: the loaded oracle to run (default load(); load_native() for the CPU baseline).
     Returns (angles [B, D], fitness [B], residual [B])."""
     c = _chain(chain)
     D = 3 * (c.shape[0] - 1)
@@ -218,7 +234,7 @@ def solve_batch(chain, targets, start_pose, particles: int, iterations: int, rng
     res = np.zeros(B, dtype=np.float32)
     lo, hi = _f32(soft_lo), _f32(soft_hi)
     bx, nb = _boxes(colliders)
-    err = load().orc_solve_batch(_p(c), c.shape[0], _p(t), _p(sp), B, int(particles), int(iterations), inertia,
+    err = (lib or load()).orc_solve_batch(_p(c), c.shape[0], _p(t), _p(sp), B, int(particles), int(iterations), inertia,
                                  local, glob, angle_weight, distance_weight, _p(pos), _p(rng), _p(ang), _p(fit),
                                  _p(res), int(threads), limit_weight, _p(lo), _p(hi), _p(bx), nb)
     if err:

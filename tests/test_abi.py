@@ -44,7 +44,7 @@ def test_compat_symbols_exported():
 
 def test_abi_version_and_strings():
     lib = _abi.load()
-    assert lib.ikpso_abi_version() == 2
+    assert lib.ikpso_abi_version() == 3
     assert lib.ikpso_status_string(0) == b"ok"
     assert lib.ikpso_status_string(2) == b"unsupported configuration"
 

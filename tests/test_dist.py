@@ -64,3 +64,25 @@ def test_gloo_world2_matches_single_process(tmp_path, oracle, total):
         got = np.load(tmp_path / f"rank{r}.npy")
         assert got.shape == (total, 23)
         assert np.array_equal(got, want)
+
+
+def test_bench_refuses_world_mismatch():
+    """Under torchrun the world is fixed by WORLD_SIZE: a different --gpus is an
+    error, not a silent one-GPU measurement (exits before touching a GPU)."""
+    import subprocess
+
+    env = dict(os.environ, WORLD_SIZE="4", RANK="0", LOCAL_RANK="0")
+    p = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "2"], env=env, capture_output=True,
+                       text=True, timeout=120)
+    assert p.returncode != 0 and "WORLD_SIZE" in p.stderr
+
+
+def test_bench_refuses_more_gpus_than_visible():
+    """--gpus N over RCCL needs N visible GPUs (none here): refused up front."""
+    import subprocess
+
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["HIP_VISIBLE_DEVICES"] = ""
+    p = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "2"], env=env, capture_output=True,
+                       text=True, timeout=120)
+    assert p.returncode != 0 and "visible GPUs" in p.stderr

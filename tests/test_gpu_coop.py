@@ -93,3 +93,74 @@ def test_auto_reports_latency_variant(device):
     s.solve(dev(wl.targets(0, 512)), iterations=5)
     assert s.kernel == "swarm_resident<ref_tree7>"
     s.close()
+
+
+# ------------------------------------------------- contention fallback
+# IKPSO_COOP_SPIN_LIMIT=0 makes every group wait give up at its first unmet poll:
+# the path a solve takes when other work on the GPU keeps a group from
+# assembling.  The solve must still complete -- restored generator states,
+# re-run on the streaming kernels -- with the results a streaming solve gives.
+
+def test_coop_forced_timeout_falls_back_batch(device, monkeypatch):
+    wl = ikpso.workload(3)
+    B, P, I = 6, 16384, 5
+    tg = dev(wl.targets(0, B))
+    out = {}
+    for name, kern, spin in (("coop", "coop", "0"), ("streaming", "streaming", None)):
+        if spin is None:
+            monkeypatch.delenv("IKPSO_COOP_SPIN_LIMIT", raising=False)
+        else:
+            monkeypatch.setenv("IKPSO_COOP_SPIN_LIMIT", spin)
+        s = ikpso.BatchSolver(wl.chain, P, pso=ikpso.PSOConfig(0.5, 0.5, 1.25, I), arith="reference", kernel=kern)
+        s.seed(B)
+        # without sync the aborted groups' swarms read as NaN ...
+        a0, f0, r0 = s.solve(tg, iterations=I, sync=False)
+        if kern == "coop":
+            torch.cuda.synchronize()
+            assert torch.isnan(f0).any() and torch.isnan(a0).any()
+            before = s.fallbacks
+            s.sync()  # ... and sync re-runs the batch from the snapshot
+            assert s.fallbacks == before + 1
+        out[name] = [t.cpu().numpy() for t in (a0, f0, r0)]
+        s.close()
+    for x, y in zip(out["coop"], out["streaming"]):
+        assert np.array_equal(x, y)
+
+
+def test_coop_forced_timeout_falls_back_compat(oracle, device, monkeypatch):
+    """calculatePSO (the visualiser's N = 16384, cooperative by AUTO) returns
+    success and the oracle's bit-exact state even when every group gives up."""
+    monkeypatch.setenv("IKPSO_ARITH", "reference")
+    monkeypatch.setenv("IKPSO_COOP_SPIN_LIMIT", "0")
+    lib = ikpso.load()
+    chain = ikpso.reference_scene(reset=True).origin.to_cuda()
+    P, I, D = 16384, 3, 21
+    parts = ikpso.particles_tensor(P, D)
+    bests = torch.zeros(P, dtype=torch.float32, device="cuda")
+    r = ikpso.rng_tensor(P)
+    assert ikpso.init_generators(r, P) == 0
+    res = np.zeros(D, dtype=np.float32)
+    before = lib.ikpso_coop_fallbacks()
+    assert ikpso.calculate_pso(parts, None, bests, r, P, chain, ikpso.PSOConfig(0.5, 0.5, 1.25, I),
+                               ikpso.MAIN_FITNESS, res) == 0
+    assert lib.ikpso_coop_fallbacks() == before + 1
+    ostate = oracle.init_generators(P, 0)
+    ores, oparts, obests = oracle.calculate_pso(chain, P, ostate, iterations=I)
+    assert np.array_equal(r.cpu().numpy()[:, :6], ostate.view(np.int32).reshape(P, 12)[:, :6])
+    assert np.array_equal(bests.cpu().numpy(), obests)
+    assert np.array_equal(parts.cpu().numpy(), oparts)
+    assert np.array_equal(res, ores)
+
+
+def test_solve_rejects_wrong_dtype_and_device(device):
+    wl = ikpso.workload(3)
+    s = ikpso.BatchSolver(wl.chain, 64)
+    s.seed(2)
+    tg = dev(wl.targets(0, 2))
+    with pytest.raises(ValueError):
+        s.solve(tg.double(), iterations=1)
+    with pytest.raises(ValueError):
+        s.solve(tg.cpu(), iterations=1)
+    with pytest.raises(ValueError):
+        s.evaluate(torch.zeros((3, 21), dtype=torch.float64, device="cuda"))
+    s.close()

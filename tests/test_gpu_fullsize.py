@@ -7,7 +7,8 @@ size-independent properties (the oracle cannot run them in test time):
   * the reported residual is the residual of the reported angles (oracle
     `checkDistance` restatement on a sample of swarms);
   * the reported fitness is the fitness of the reported angles (oracle
-    restatement of calculateDistance on the sample; FAST tolerance 1e-5);
+    restatement of calculateDistance on the sample, config 5's soft
+    joint-limit penalty included; FAST tolerance 1e-5);
   * answers are finite and inside the joint limits.
 """
 import numpy as np
@@ -57,6 +58,6 @@ def test_fullsize_shards_match_one_launch(oracle, device, config, world):
         ch["target_position"][eff] = tg[b]  # the swarm's own targets
         r = oracle.residual(ch, ang[b])
         assert abs(float(r) - float(res[b])) <= 1e-4 + 1e-5 * abs(float(r)), (b, r, res[b])
-        if config == 4:
-            f = oracle.fitness(ch, ang[b])
-            assert abs(float(f) - float(fit[b])) <= 1e-5 * abs(float(f)) + 1e-6, (b, f, fit[b])
+        # the reported fitness, soft joint-limit penalty included (config 5)
+        f = oracle.fitness(ch, ang[b], limit_weight=wl.limit_weight, soft_lo=wl.soft_lo, soft_hi=wl.soft_hi)
+        assert abs(float(f) - float(fit[b])) <= 1e-5 * abs(float(f)) + 1e-6, (b, f, fit[b])

@@ -159,7 +159,9 @@ def test_tier_a(oracle, device, scene_chain, monkeypatch, arith, P, I, kernel):
 
 
 def test_tier_b_config1_and_2(oracle, device, scene_chain, monkeypatch):
-    """Chaotic regime: final fitness/residual statistically equal over several seeds."""
+    """Chaotic regime, single solves through calculatePSO: final fitness and
+    residual statistically equal over several seeds (the batched >= 64-swarm
+    check is test_tier_b_config3_batch)."""
     for (P, I, seeds) in ((256, 200, 8), (1024, 500, 4)):
         gf, of_, gr, orr = [], [], [], []
         for k in range(seeds):
@@ -170,10 +172,96 @@ def test_tier_b_config1_and_2(oracle, device, scene_chain, monkeypatch):
             gf.append(bests.min()), of_.append(obests.min())
             gr.append(oracle.residual(scene_chain, res)), orr.append(oracle.residual(scene_chain, ores))
         gf, of_ = np.array(gf), np.array(of_)
-        rel = np.abs(gf - of_) / of_
-        assert np.mean(rel <= 1e-3) >= 0.75, (P, I, rel)
-        assert abs(gf.mean() - of_.mean()) / of_.mean() < 5e-3
+        assert abs(gf.mean() - of_.mean()) / of_.mean() < 5e-3, (P, I, gf, of_)
         assert abs(np.mean(gr) - np.mean(orr)) < 1e-3 + 0.01 * np.mean(orr)
+
+
+TIER_B_SWARMS = 64
+
+
+@pytest.fixture(scope="module")
+def tier_b_case(oracle):
+    """SURVEY.md §8(c) tier B on BASELINE config 3: 64 swarms x 1024 particles x
+    500 iterations, the oracle parallel over the host's cores."""
+    wl = ikpso.workload(3)
+    B, P, I = TIER_B_SWARMS, wl.particles, wl.iterations
+    tg = wl.targets(0, B)
+    ostate = oracle.init_generators(B * P, 0)
+    oang, ofit, ores = oracle.solve_batch(wl.chain, tg, None, P, I, ostate, threads=0)
+    return wl, tg, oang, ofit, ores, ostate
+
+
+@pytest.mark.parametrize("arith", ["fast", "reference"])
+def test_tier_b_config3_batch(oracle, device, tier_b_case, arith):
+    """Tier B: >= 90 % of the 64 swarms within |df|/f <= 1e-3 of the oracle's
+    gbest fitness, mean gbest fitness within 0.5 %, mean residual within 1e-3 +
+    1 %; the generator states after 500 iterations are bit-exact (draw count).
+    REFERENCE arithmetic: every swarm bit-exact."""
+    wl, tg, oang, ofit, ores, ostate = tier_b_case
+    B, P, I = TIER_B_SWARMS, wl.particles, wl.iterations
+    s = ikpso.BatchSolver(wl.chain, P, pso=wl.pso, arith=arith, kernel="resident")
+    s.seed(B)
+    ang, fit, res = (t.cpu().numpy() for t in s.solve(dev(tg), iterations=I))
+    s.close()
+    if arith == "reference":
+        assert np.array_equal(ang, oang) and np.array_equal(fit, ofit)
+        return
+    rel = np.abs(fit - ofit) / ofit
+    frac = float(np.mean(rel <= 1e-3))
+    print(f"tier B config 3: {frac:.3f} of {B} swarms within 1e-3; median |df|/f {np.median(rel):.2e}, "
+          f"max {rel.max():.2e}; mean fitness {fit.mean():.6f} vs {ofit.mean():.6f}")
+    assert frac >= 0.9, (frac, np.sort(rel)[-8:])
+    assert abs(fit.mean() - ofit.mean()) / ofit.mean() < 5e-3
+    assert abs(res.mean() - ores.mean()) < 1e-3 + 0.01 * ores.mean()
+
+
+# --------------------------------------------------------------- tie-breaking
+def tie_chain():
+    """The reference tree with every angle pinned at 0 (lo = hi = 0) except the
+    X angle of leaf node 7, free in [-0.1, 0.1].  With the other two angles of
+    node 7 at 0 the link direction does not depend on it, so it moves no node;
+    with a NEGATIVE angle weight the fitness is C - (3/7)·a^2, minimal at both
+    a = +0.1 and a = -0.1 -- exactly equal values, different vectors.  Particles
+    pushed onto either bound by the clamp tie for the swarm minimum, and the
+    global best must be the lowest-index one (thrust::min_element,
+    src/kernel.cu:297,315)."""
+    ch = ikpso.reference_scene(reset=True).origin.to_cuda()
+    ch["rotation"][1:] = 0.0
+    ch["min_rotation"][1:] = 0.0
+    ch["max_rotation"][1:] = 0.0
+    ch["min_rotation"][7, 0] = -0.1
+    ch["max_rotation"][7, 0] = 0.1
+    return ch
+
+
+@pytest.mark.parametrize("kernel,P", [("resident", 1024), ("auto", 1024), ("coop", 16384), ("streaming", 3000)])
+@pytest.mark.parametrize("arith", ["reference", "fast"])
+def test_tie_break_lowest_index(oracle, device, monkeypatch, kernel, P, arith):
+    monkeypatch.setenv("IKPSO_ARITH", arith)
+    monkeypatch.setenv("IKPSO_KERNEL", kernel)
+    chain = tie_chain()
+    D = 21
+    fit_cfg = ikpso.FitnessConfig(-3.0, 0.0, 0.1)
+    for I in (1, 6):
+        parts = ikpso.particles_tensor(P, D)
+        bests = torch.zeros(P, dtype=torch.float32, device="cuda")
+        r = ikpso.rng_tensor(P)
+        assert ikpso.init_generators(r, P) == 0
+        res = np.zeros(D, dtype=np.float32)
+        assert ikpso.calculate_pso(parts, None, bests, r, P, chain, ikpso.PSOConfig(0.5, 0.5, 1.25, I), fit_cfg,
+                                   res) == 0
+        b = bests.cpu().numpy()
+        pb = parts.cpu().numpy()[2]  # [D][P] local bests
+        ties = np.flatnonzero(b == b.min())
+        signs = np.sign(pb[18, ties])
+        assert len(ties) > 10 and (signs > 0).any() and (signs < 0).any(), "the case must hold real ties"
+        if I == 1:  # the global best is the first minimum of this iteration's local bests
+            assert np.array_equal(res, pb[:, ties[0]]), (ties[:4], res[18], pb[18, ties[:4]])
+        ostate = oracle.init_generators(P, 0)
+        ores, oparts, obests = oracle.calculate_pso(chain, P, ostate, iterations=I, angle_weight=-3.0)
+        assert np.array_equal(res, ores), (I, res[18], ores[18])
+        if arith == "reference":
+            assert np.array_equal(b, obests) and np.array_equal(parts.cpu().numpy(), oparts)
 
 
 def test_distance_weight_term(oracle, device, monkeypatch):
