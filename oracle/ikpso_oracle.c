@@ -252,19 +252,54 @@ typedef struct {
     /* collider term (src/kernel.cu:104-136; ikpso_gjk.c): obj_t[collider_count] */
     const void* colliders;
     int collider_count;
+    /* Joint-axis mask -- an EXTENSION, not in the
+     * reference: axis_mask[k] (k = 1..J; entry 0 ignored) has bit c set when
+     * Euler angle c of node k is a PSO dimension.  A locked axis keeps the
+     * node's rotation[c] (its rest value) and takes no draws and no update; the
+     * particle state, the draws, the clamp, the soft penalty, start poses and
+     * results cover the D free dimensions only, in node order, axis order
+     * within a node.  The fitness is the reference's calculateDistance of the
+     * full Euler vector (locked entries add exact zeros to the angle term).
+     * NULL = every axis free = the reference. */
+    const uint8_t* axis_mask;
 } orc_extra;
+
+/* Free-dimension map of a chain: fd[d] = Euler index 3*(k-1)+c of free
+ * dimension d; returns D. */
+static int free_dims(const orc_extra* ex, int node_count, int* fd)
+{
+    int D = 0;
+    for (int k = 1; k < node_count; k++)
+        for (int c = 0; c < 3; c++)
+            if (!ex || !ex->axis_mask || ((ex->axis_mask[k] >> c) & 1)) fd[D++] = 3 * (k - 1) + c;
+    return D;
+}
 
 /* ikpso_gjk.c */
 int orc_node_collides(const float* node, const float* parent, float length, const void* colliders, int count);
 
-static float penalty_term(const orc_extra* pen, const float* angles, int dof)
+/* angles: the full Euler vector; soft_lo/soft_hi: per free dimension */
+static float penalty_term(const orc_extra* pen, const float* angles, int node_count)
 {
+    int fd[3 * 64];
+    const int D = free_dims(pen, node_count, fd);
     float p = 0.0f;
-    for (int d = 0; d < dof; d++) {
-        float over = fmaxf(fmaxf(angles[d] - pen->soft_hi[d], pen->soft_lo[d] - angles[d]), 0.0f);
+    for (int d = 0; d < D; d++) {
+        const float a = angles[fd[d]];
+        float over = fmaxf(fmaxf(a - pen->soft_hi[d], pen->soft_lo[d] - a), 0.0f);
         p = p + over * over;
     }
     return pen->limit_weight * p;
+}
+
+/* Full Euler vector of a chain from its free dimensions (locked axes at rest). */
+static void expand_angles(const orc_node* chain, int node_count, const orc_extra* ex, const float* x, float* full)
+{
+    int fd[3 * 64];
+    const int D = free_dims(ex, node_count, fd);
+    for (int k = 1; k < node_count; k++)
+        for (int c = 0; c < 3; c++) full[3 * (k - 1) + c] = chain[k].rotation[c];
+    for (int d = 0; d < D; d++) full[fd[d]] = x[d];
 }
 
 static float fitness_pen(const orc_node* chain, int node_count, const float* positions, const float* angles,
@@ -282,7 +317,7 @@ float orc_fitness_ex(const orc_node* chain, int node_count, const float* positio
                      float angle_weight, float distance_weight, float limit_weight, const float* soft_lo,
                      const float* soft_hi, const void* colliders, int collider_count)
 {
-    orc_extra pen = {limit_weight, soft_lo, soft_hi, colliders, collider_count};
+    orc_extra pen = {limit_weight, soft_lo, soft_hi, colliders, collider_count, NULL};
     return fitness_pen(chain, node_count, positions, angles, angle_weight, distance_weight, &pen);
 }
 
@@ -325,16 +360,31 @@ static float fitness_pen(const orc_node* chain, int node_count, const float* pos
     if (mp != mats) free(mp);
     const float jn = (float)(dof / 3);
     float f = distance + distance_weight / jn * pos_diff + angle_weight / jn * rot_diff;
-    if (pen && pen->limit_weight != 0.0f && pen->soft_lo && pen->soft_hi) f = f + penalty_term(pen, angles, dof);
+    if (pen && pen->limit_weight != 0.0f && pen->soft_lo && pen->soft_hi) f = f + penalty_term(pen, angles, node_count);
     return f;
 }
 
+/* calculateDistance of a masked chain: angles = the D free dimensions. */
+float orc_fitness_mask(const orc_node* chain, int node_count, const float* positions, const float* angles,
+                       float angle_weight, float distance_weight, float limit_weight, const float* soft_lo,
+                       const float* soft_hi, const void* colliders, int collider_count, const uint8_t* axis_mask)
+{
+    orc_extra pen = {limit_weight, soft_lo, soft_hi, colliders, collider_count, axis_mask};
+    float full[3 * 64];
+    if (node_count > 64) return NAN;
+    expand_angles(chain, node_count, &pen, angles, full);
+    return fitness_pen(chain, node_count, positions, full, angle_weight, distance_weight, &pen);
+}
+
+/* particles: [3][D][count] over the free dimensions */
 static float fitness_soa(const orc_node* chain, int node_count, const float* positions, const float* particles,
                          int64_t count, int64_t i, float aw, float dw, const orc_extra* pen)
 {
-    const int dof = 3 * (node_count - 1);
-    float ang[3 * 64];
-    for (int d = 0; d < dof; d++) ang[d] = particles[pidx(count, i, 0, d, dof)];
+    int fd[3 * 64];
+    const int D = free_dims(pen, node_count, fd);
+    float x[3 * 64], ang[3 * 64];
+    for (int d = 0; d < D; d++) x[d] = particles[pidx(count, i, 0, d, D)];
+    expand_angles(chain, node_count, pen, x, ang);
     return fitness_pen(chain, node_count, positions, ang, aw, dw, pen);
 }
 
@@ -399,7 +449,7 @@ int orc_calculate_pso_ex(float* particles, const float* positions, float* bests,
                          float limit_weight, const float* soft_lo, const float* soft_hi, const void* colliders,
                          int collider_count)
 {
-    orc_extra pen = {limit_weight, soft_lo, soft_hi, colliders, collider_count};
+    orc_extra pen = {limit_weight, soft_lo, soft_hi, colliders, collider_count, NULL};
     return calculate_pso_pen(particles, positions, bests, randoms, size, chain, node_count, inertia, local, global,
                              iterations, angle_weight, distance_weight, result, &pen);
 }
@@ -409,16 +459,16 @@ static int calculate_pso_pen(float* particles, const float* positions, float* be
                              float global, int iterations, float angle_weight, float distance_weight,
                              float* result, const orc_extra* pen)
 {
-    const int dof = 3 * (node_count - 1);
+    /* dof = the free dimensions (3 per node without an axis mask, the reference) */
+    int fd[3 * 64];
+    const int dof = free_dims(pen, node_count, fd);
     const int64_t n = size;
 
     /* initParticlesKernel (src/kernel.cu:223-266) */
     for (int64_t i = 0; i < n; i++) {
-        for (int d = 0; d < dof; d += 3) {
-            int ci = d / 3 + 1;
-            particles[pidx(n, i, 0, d + 0, dof)] = chain[ci].rotation[0];
-            particles[pidx(n, i, 0, d + 1, dof)] = chain[ci].rotation[1];
-            particles[pidx(n, i, 0, d + 2, dof)] = chain[ci].rotation[2];
+        for (int d = 0; d < dof; d++) {
+            const int ci = fd[d] / 3 + 1;
+            particles[pidx(n, i, 0, d, dof)] = chain[ci].rotation[fd[d] % 3];
         }
         for (int d = 0; d < dof; d++) {
             particles[pidx(n, i, 1, d, dof)] = orc_curand_uniform(&randoms[i]) * 2.0f - 1.0f;
@@ -445,12 +495,10 @@ static int calculate_pso_pen(float* particles, const float* positions, float* be
                                 global * r3 * (result[d] - particles[xi]);
                 particles[xi] += particles[vi];
             }
-            for (int k = 1; k <= dof / 3; k++) {
-                int d = (k - 1) * 3;
-                for (int c = 0; c < 3; c++) {
-                    int64_t xi = pidx(n, i, 0, d + c, dof);
-                    particles[xi] = clampf_ref(particles[xi], chain[k].min_rotation[c], chain[k].max_rotation[c]);
-                }
+            for (int d = 0; d < dof; d++) {
+                const int k = fd[d] / 3 + 1, c = fd[d] % 3;
+                int64_t xi = pidx(n, i, 0, d, dof);
+                particles[xi] = clampf_ref(particles[xi], chain[k].min_rotation[c], chain[k].max_rotation[c]);
             }
         }
         /* updateLocalBests (src/kernel.cu:202-221) */
@@ -481,6 +529,13 @@ static int calculate_pso_pen(float* particles, const float* positions, float* be
  * limit_weight/soft_lo/soft_hi: optional penalty extension (0/NULL = off).
  * colliders/collider_count: obj_t boxes of the collider term (0 = off).
  * Parallel over swarms with OpenMP (threads <= 0: runtime default). */
+int orc_solve_batch_mask(const orc_node* chain, int node_count, const float* targets, const float* start_pose,
+                         int64_t num_swarms, int particles_per_swarm, int iterations, float inertia, float local,
+                         float global, float angle_weight, float distance_weight, const float* positions,
+                         orc_rng* rng, float* out_angles, float* out_fitness, float* out_residual, int threads,
+                         float limit_weight, const float* soft_lo, const float* soft_hi, const void* colliders,
+                         int collider_count, const uint8_t* axis_mask);
+
 int orc_solve_batch(const orc_node* chain, int node_count, const float* targets, const float* start_pose,
                     int64_t num_swarms, int particles_per_swarm, int iterations, float inertia, float local,
                     float global, float angle_weight, float distance_weight, const float* positions,
@@ -488,13 +543,29 @@ int orc_solve_batch(const orc_node* chain, int node_count, const float* targets,
                     float limit_weight, const float* soft_lo, const float* soft_hi, const void* colliders,
                     int collider_count)
 {
-    const int dof = 3 * (node_count - 1);
+    return orc_solve_batch_mask(chain, node_count, targets, start_pose, num_swarms, particles_per_swarm, iterations,
+                                inertia, local, global, angle_weight, distance_weight, positions, rng, out_angles,
+                                out_fitness, out_residual, threads, limit_weight, soft_lo, soft_hi, colliders,
+                                collider_count, NULL);
+}
+
+/* axis_mask: see orc_extra (NULL = the reference); start_pose [B][D], out_angles [B][D]
+ * over the D free dimensions. */
+int orc_solve_batch_mask(const orc_node* chain, int node_count, const float* targets, const float* start_pose,
+                         int64_t num_swarms, int particles_per_swarm, int iterations, float inertia, float local,
+                         float global, float angle_weight, float distance_weight, const float* positions,
+                         orc_rng* rng, float* out_angles, float* out_fitness, float* out_residual, int threads,
+                         float limit_weight, const float* soft_lo, const float* soft_hi, const void* colliders,
+                         int collider_count, const uint8_t* axis_mask)
+{
     const int64_t P = particles_per_swarm;
-    orc_extra pen = {limit_weight, soft_lo, soft_hi, colliders, collider_count};
+    orc_extra pen = {limit_weight, soft_lo, soft_hi, colliders, collider_count, axis_mask};
     const orc_extra* penp = &pen;
+    if (node_count > 64 || node_count < 2) return 1;
+    int fd[3 * 64];
+    const int dof = free_dims(penp, node_count, fd);
     int num_eff = 0;
     for (int k = 1; k < node_count; k++) num_eff += chain[k].node_type == ORC_EFFECTOR;
-    if (node_count > 64 || node_count < 2) return 1;
     int err = 0;
 #ifdef _OPENMP
     if (threads > 0) omp_set_num_threads(threads);
@@ -514,10 +585,10 @@ int orc_solve_batch(const orc_node* chain, int node_count, const float* targets,
             continue;
         }
         memcpy(lc, chain, sizeof(orc_node) * node_count);
+        if (start_pose)
+            for (int d = 0; d < dof; d++) lc[fd[d] / 3 + 1].rotation[fd[d] % 3] = start_pose[b * dof + d];
         int e = 0;
         for (int k = 1; k < node_count; k++) {
-            if (start_pose)
-                for (int c = 0; c < 3; c++) lc[k].rotation[c] = start_pose[b * dof + 3 * (k - 1) + c];
             if (lc[k].node_type == ORC_EFFECTOR) {
                 if (targets)
                     for (int c = 0; c < 3; c++) lc[k].target_position[c] = targets[(b * num_eff + e) * 3 + c];
@@ -531,7 +602,11 @@ int orc_solve_batch(const orc_node* chain, int node_count, const float* targets,
         for (int64_t i = 1; i < P; i++)
             if (bests[i] < gmin) gmin = bests[i];
         out_fitness[b] = gmin;
-        if (out_residual) out_residual[b] = orc_residual(lc, node_count, res);
+        if (out_residual) {
+            float full[3 * 64];
+            expand_angles(lc, node_count, penp, res, full);
+            out_residual[b] = orc_residual(lc, node_count, full);
+        }
         free(parts);
         free(bests);
     }

@@ -95,6 +95,14 @@ def _bind(lib):
             [_P, _P, _P, _P, ctypes.c_int64, _P, ctypes.c_int, ctypes.c_float, ctypes.c_float, ctypes.c_float,
              ctypes.c_int, ctypes.c_float, ctypes.c_float, _P, ctypes.c_float, _P, _P, _P, ctypes.c_int],
         ),
+        "orc_fitness_mask": (ctypes.c_float, [_P, ctypes.c_int, _P, _P, ctypes.c_float, ctypes.c_float,
+                                              ctypes.c_float, _P, _P, _P, ctypes.c_int, _P]),
+        "orc_solve_batch_mask": (
+            ctypes.c_int,
+            [_P, ctypes.c_int, _P, _P, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_float,
+             ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float, _P, _P, _P, _P, _P, ctypes.c_int,
+             ctypes.c_float, _P, _P, _P, ctypes.c_int, _P],
+        ),
         "orc_solve_batch": (
             ctypes.c_int,
             [_P, ctypes.c_int, _P, _P, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_float,
@@ -192,6 +200,43 @@ def fitness(chain, angles, angle_weight=3.0, distance_weight=0.0, positions=None
                                             limit_weight, _p(lo), _p(hi), _p(bx), nb))
 
 
+def _mask(axis_mask, node_count):
+    if axis_mask is None:
+        return None
+    m = np.ascontiguousarray(axis_mask, dtype=np.uint8)
+    if m.shape != (node_count,):
+        raise ValueError(f"axis_mask must have one entry per node ({node_count})")
+    return m
+
+
+def free_dims(chain, axis_mask=None) -> np.ndarray:
+    """Euler indices 3*(k-1)+c of the free dimensions of a (masked) chain."""
+    c = _chain(chain)
+    m = _mask(axis_mask, c.shape[0])
+    return np.array([3 * (k - 1) + a for k in range(1, c.shape[0]) for a in range(3)
+                     if m is None or (m[k] >> a) & 1], dtype=np.int64)
+
+
+def expand(chain, angles, axis_mask=None) -> np.ndarray:
+    """Full Euler vector of a masked chain from its free dimensions (locked axes at rest)."""
+    c = _chain(chain)
+    full = np.asarray(c["rotation"][1:], dtype=np.float32).reshape(-1).copy()
+    full[free_dims(c, axis_mask)] = np.asarray(angles, dtype=np.float32)
+    return full
+
+
+def fitness_mask(chain, angles, axis_mask, angle_weight=3.0, distance_weight=0.0, positions=None,
+                 limit_weight=0.0, soft_lo=None, soft_hi=None, colliders=None) -> np.float32:
+    """calculateDistance of a masked chain; angles = its free dimensions."""
+    c = _chain(chain)
+    a = _f32(angles)
+    pos, lo, hi = _f32(positions), _f32(soft_lo), _f32(soft_hi)
+    bx, nb = _boxes(colliders)
+    m = _mask(axis_mask, c.shape[0])
+    return np.float32(load().orc_fitness_mask(_p(c), c.shape[0], _p(pos), _p(a), angle_weight, distance_weight,
+                                              limit_weight, _p(lo), _p(hi), _p(bx), nb, _p(m)))
+
+
 def residual(chain, angles) -> np.float32:
     c = _chain(chain)
     a = np.ascontiguousarray(angles, dtype=np.float32)
@@ -219,12 +264,15 @@ def calculate_pso(chain, size: int, randoms: np.ndarray, inertia=0.5, local=0.5,
 
 def solve_batch(chain, targets, start_pose, particles: int, iterations: int, rng: np.ndarray, inertia=0.5,
                 local=0.5, glob=1.25, angle_weight=3.0, distance_weight=0.0, positions=None, threads: int = 0,
-                limit_weight=0.0, soft_lo=None, soft_hi=None, colliders=None, lib=None):
+                limit_weight=0.0, soft_lo=None, soft_hi=None, colliders=None, lib=None, axis_mask=None):
     """B independent reference solves (OpenMP over swarms).  rng: [B*P] states, advanced in place.
     lib: the loaded oracle to run (default load(); load_native() for the CPU baseline).
+    axis_mask: [node_count] uint8, bit c = Euler angle c of node k is free (None: all; the
+    reference); D = the free dimensions, start_pose / angles / soft limits over those.
     Returns (angles [B, D], fitness [B], residual [B])."""
     c = _chain(chain)
-    D = 3 * (c.shape[0] - 1)
+    m = _mask(axis_mask, c.shape[0])
+    D = len(free_dims(c, m))
     t = np.ascontiguousarray(targets, dtype=np.float32)
     B = t.shape[0]
     sp = None if start_pose is None else np.ascontiguousarray(start_pose, dtype=np.float32)
@@ -234,9 +282,10 @@ def solve_batch(chain, targets, start_pose, particles: int, iterations: int, rng
     res = np.zeros(B, dtype=np.float32)
     lo, hi = _f32(soft_lo), _f32(soft_hi)
     bx, nb = _boxes(colliders)
-    err = (lib or load()).orc_solve_batch(_p(c), c.shape[0], _p(t), _p(sp), B, int(particles), int(iterations), inertia,
-                                 local, glob, angle_weight, distance_weight, _p(pos), _p(rng), _p(ang), _p(fit),
-                                 _p(res), int(threads), limit_weight, _p(lo), _p(hi), _p(bx), nb)
+    err = (lib or load()).orc_solve_batch_mask(
+        _p(c), c.shape[0], _p(t), _p(sp), B, int(particles), int(iterations), inertia, local, glob, angle_weight,
+        distance_weight, _p(pos), _p(rng), _p(ang), _p(fit), _p(res), int(threads), limit_weight, _p(lo), _p(hi),
+        _p(bx), nb, _p(m))
     if err:
         raise RuntimeError(f"orc_solve_batch failed ({err})")
     return ang, fit, res
