@@ -39,10 +39,11 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", type=int, default=3, choices=[2, 3, 4, 5],
+    ap.add_argument("--config", default="3", choices=["2", "3", "4", "5", "dh7", "dh7-nofold", "dh7-locked"],
                     help="BASELINE config: 2 = one swarm (latency), 3 = 4096 targets per GPU (default), "
                          "4 = 65536 targets over all GPUs, 5 = 20-joint chain, 8192 targets over all GPUs, "
-                         "4096 particles, penalty")
+                         "4096 particles, penalty; dh7* = the 7-joint iiwa DH arm, 4096 targets per GPU, with "
+                         "its joint-axis mask (dh7: folded chain; dh7-nofold: Euler kernels) or locked axes")
     ap.add_argument("--swarms-per-gpu", type=int, default=None)
     ap.add_argument("--particles", type=int, default=None)
     ap.add_argument("--iterations", type=int, default=None)
@@ -138,7 +139,7 @@ def _cpu_sample(oracle, lib, wl, P, I, first, threads, seconds, max_batches, kw)
     return done, time.perf_counter() - t0
 
 
-def cpu_baseline(seconds: float, threads: int):
+def cpu_baseline(seconds: float, threads: int, dh=None):
     """The CPU oracle (the reference algorithm restated in C, reference 4x4 FK
     order, -ffp-contract=off) built -O3 -march=native on this host, OpenMP over
     swarms, on bounded samples of configs 3 and 5 (BASELINE.md
@@ -173,7 +174,13 @@ def cpu_baseline(seconds: float, threads: int):
     I5 = 10
     kw5 = {"limit_weight": w5.limit_weight, "soft_lo": w5.soft_lo, "soft_hi": w5.soft_hi}
     d5, e5 = _cpu_sample(oracle, lib, w5, w5.particles, I5, 0, threads, seconds / 2, 16, kw5)
-    return {"value": ups, "unit": "particle-updates/s", "cores": threads, "kind": "port",
+    dhres = None
+    if dh is not None:  # the DH workload itself (axis mask as the GPU run; the oracle has one FK form)
+        kwd = {"axis_mask": dh.axis_mask, "angle_weight": dh.fit.angle_weight}
+        dd, ed = _cpu_sample(oracle, lib, dh, dh.particles, 50, 0, threads, seconds / 2, 16, kwd)
+        dhres = {"value": dd * dh.particles * 50 / ed, "unit": "particle-updates/s", "cores": threads,
+                 "sample": f"{dd} swarms x {dh.particles} particles x 50 iterations of {dh.name}, {ed:.1f} s"}
+    return {"value": ups, "unit": "particle-updates/s", "cores": threads, "kind": "port", "dh": dhres,
             "solves_per_s": done / el, "value_1thread": d1 * P * I / e1, "build": build, **facts,
             "by_threads": {str(n): round(v[0]) for n, v in runs.items()},
             "sample": f"{done} swarms x {P} particles x {I} iterations of config 3 (same targets/seeds), "
@@ -207,20 +214,21 @@ def main():
     dev = torch.device("cuda", torch.cuda.current_device())
 
     wl = ikpso.workload(args.config)
+    cfg = int(args.config) if args.config.isdigit() else args.config
     P = args.particles or wl.particles
     I = args.iterations or wl.iterations
     if args.swarms_per_gpu:
         Bl = args.swarms_per_gpu
-    elif args.config == 3:
+    elif cfg == 3 or not isinstance(cfg, int):
         Bl = wl.swarms                      # weak scaling: 4096 per GPU
     else:
         Bl = -(-wl.swarms // world)         # configs 4/5: the named total over all GPUs
     total = Bl * world
     first = rank * Bl
     targets = torch.from_numpy(wl.targets(first, Bl)).to(dev)
-    solver = ikpso.BatchSolver(wl.chain, P, pso=ikpso.PSOConfig(0.5, 0.5, 1.25, I), arith=args.arith,
+    solver = ikpso.BatchSolver(wl.chain, P, pso=ikpso.PSOConfig(0.5, 0.5, 1.25, I), fit=wl.fit, arith=args.arith,
                                limit_weight=wl.limit_weight, soft_lo=wl.soft_lo, soft_hi=wl.soft_hi,
-                               kernel=args.kernel)
+                               kernel=args.kernel, axis_mask=wl.axis_mask, fold=wl.fold)
     solver.seed(Bl, seed_base=0, first_swarm=first)
     D = solver.dof
     out = (torch.empty((Bl, D), device=dev), torch.empty((Bl,), device=dev), torch.empty((Bl,), device=dev))
@@ -268,8 +276,9 @@ def main():
     mean_res = float(res[:, D + 1].mean())
 
     single_ms = None
-    if rank == 0 and args.config != 5:
-        s2 = ikpso.BatchSolver(wl.chain, P, pso=ikpso.PSOConfig(0.5, 0.5, 1.25, I), arith=args.arith)
+    if rank == 0 and cfg != 5:
+        s2 = ikpso.BatchSolver(wl.chain, P, pso=ikpso.PSOConfig(0.5, 0.5, 1.25, I), fit=wl.fit, arith=args.arith,
+                               axis_mask=wl.axis_mask, fold=wl.fold)
         s2.seed(1)
         tg1 = targets[:1].contiguous()
         s2.solve(tg1, iterations=I)
@@ -323,13 +332,18 @@ def main():
             },
         }
         cpu = None
-        if world == 1 and args.cpu_seconds > 0 and args.config in (3, 5):
-            cpu = cpu_baseline(args.cpu_seconds, args.cpu_threads)
-            if args.config == 5:  # the config-5 figure is this line's baseline
+        if world == 1 and args.cpu_seconds > 0 and cfg in (3, 5, "dh7", "dh7-nofold", "dh7-locked"):
+            cpu = cpu_baseline(args.cpu_seconds, args.cpu_threads, dh=wl if isinstance(cfg, str) else None)
+            if cfg == 5:  # the config-5 figure is this line's baseline
                 cpu = dict(cpu, value=cpu["config5"]["value"], sample=cpu["config5"]["sample"])
+            if isinstance(cfg, str):  # the DH arm's own figure
+                cpu = dict(cpu, value=cpu["dh"]["value"], sample=cpu["dh"]["sample"])
+        metric = {5: "PSO particle-updates/sec + IK solves/sec, 20-DOF 4096-particle swarm (config 5)"}.get(
+            cfg, "PSO particle-updates/sec + IK solves/sec, 7-DOF 1024-particle swarm")
+        if isinstance(cfg, str):
+            metric += f" ({cfg}: 7-joint DH arm, D = {D})"
         line = {
-            "metric": "PSO particle-updates/sec + IK solves/sec, 7-DOF 1024-particle swarm" if args.config != 5
-                      else "PSO particle-updates/sec + IK solves/sec, 20-DOF 4096-particle swarm (config 5)",
+            "metric": metric,
             "value": value,
             "unit": "particle-updates/s",
             "n_gpus": world,
@@ -342,9 +356,10 @@ def main():
             "dtype": "f32",
             "data": {2: "the reference scene's reset targets (src/Main.cpp:334-336)",
                      5: "synthetic (seeded targets uniform in a radius-2..4 shell)"}.get(
-                args.config, "synthetic (seeded targets: reset targets + U[-0.25,0.25]^3 per effector)"),
+                cfg, "synthetic (seeded reachable targets: the arm's tool positions at seeded joint angles)"
+                if isinstance(cfg, str) else "synthetic (seeded targets: reset targets + U[-0.25,0.25]^3 per effector)"),
             "config": {
-                "workload": f"config{args.config}: {wl.description}; {P} particles, {I} PSO iterations, "
+                "workload": f"{wl.name}: {wl.description}; {P} particles, {I} PSO iterations, "
                             f"{Bl} targets per GPU ({total} total)",
                 "swarms_per_gpu": Bl, "total_swarms": total, "particles": P, "iterations": I, "dof": D,
                 "parallelism": f"dp{world} (swarm shards) + {'RCCL' if args.dist_backend == 'nccl' else 'gloo (rehearsal)'}"
@@ -360,7 +375,7 @@ def main():
         }
         if valu:
             line["roofline"]["valu"] = valu
-        if args.config == 2:
+        if cfg == 2:
             line["roofline"]["note"] = ("config 2 is one swarm on 4 of 256 CUs: latency-bound (SURVEY 8(d)), "
                                         "the chip-wide fraction is not a kernel-quality figure")
         print(json.dumps(line), flush=True)

@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define IKPSO_ABI_VERSION 3
+#define IKPSO_ABI_VERSION 4
 
 typedef int ikpso_status;
 enum {
@@ -163,6 +163,18 @@ typedef struct ikpso_solver_desc {
     const ikpso_collider* colliders; /* any, [collider_count] or NULL */
     int32_t collider_count;
     int32_t flags;            /* IKPSO_FLAG_* */
+    /* Joint-axis mask (ABI >= 4; an extension -- the reference hard-wires three
+     * Euler axes per node, src/kernel.cu:52-56,160-187): any, [node_count] or
+     * NULL.  Bit c of axis_mask[k] set = Euler angle c of node k is a PSO
+     * dimension; a clear bit locks that angle at the node's rotation[c] (no
+     * draws, no update, no clamp; the angle term sees an exact zero).  Entry 0
+     * (the origin) is ignored.  NULL = every axis free = the reference.  D, the
+     * solver's dimension count, is then the number of free axes: start poses,
+     * answers, soft limits and evaluate()'s angles carry those D values in node
+     * order, axis order within a node.  FAST solves of a serial chain with a
+     * tip effector and no distance/collider term run on the chain folded into
+     * its free axes (one sincos per free angle; DH arms); see IKPSO_FLAG_NO_FOLD. */
+    const uint8_t* axis_mask;
 } ikpso_solver_desc;
 
 /* ikpso_solver_desc.flags (env IKPSO_POSREF=node_slot for ikpso_calculate_pso). */
@@ -172,7 +184,10 @@ enum {
      * which FillPositions (src/Node.h:110-149) filled with node k-2's; with
      * this flag positions is [4*(J+2)] as FillPositions writes it and node k
      * reads slot k+1, its own.  Off: bit-compatible with the reference. */
-    IKPSO_FLAG_POSREF_NODE_SLOT = 1
+    IKPSO_FLAG_POSREF_NODE_SLOT = 1,
+    /* Solve a masked chain with the Euler kernels (locked axes skipped) even
+     * where the folded form applies (ABI >= 4; comparisons and tests). */
+    IKPSO_FLAG_NO_FOLD = 2
 };
 
 ikpso_status ikpso_solver_create(const ikpso_solver_desc* desc, ikpso_solver** out);
@@ -217,12 +232,15 @@ int64_t ikpso_coop_fallbacks(void);
 /* Evaluate the device FK + fitness for n angle vectors (no PSO):
  *   angles device [n][D]; targets device [n][E][3] or NULL (chain targets);
  *   rest device [n][D] or NULL (chain rotations); out_fitness device [n] or NULL;
- *   out_positions device [n][J][3] or NULL (world position of nodes 1..J). */
+ *   out_positions device [n][J][3] or NULL (world position of nodes 1..J).
+ *   D = free dimensions (the axis mask); locked angles at the chain's rotation.
+ *   Always the Euler form of the chain (a folded FAST solver's answers agree
+ *   with it within the FAST tolerance). */
 ikpso_status ikpso_solver_evaluate(ikpso_solver* solver, const float* angles, const float* targets,
                                    const float* rest, int64_t n, float* out_fitness, float* out_positions,
                                    void* stream);
 
-/* Introspection. */
+/* Introspection.  dof = D, the free dimensions. */
 int ikpso_solver_dof(const ikpso_solver* solver);
 int ikpso_solver_effectors(const ikpso_solver* solver);
 /* Name of the kernel variant the solver dispatches to (family / topology); after a

@@ -8,6 +8,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <array>
 #include <atomic>
 #include <mutex>
 #include <new>
@@ -129,7 +130,58 @@ struct Extras {
     // IKPSO_FLAG_POSREF_NODE_SLOT: positions[] is [4*(J+2)] and node k's
     // reference position is read from slot k+1 (where FillPositions wrote it)
     bool posref_node_slot = false;
+    const uint8_t* axis_mask = nullptr;  // host copy, [J + 1] (entry 0 ignored), or null
 };
+
+// ---- the folded serial chain (TopoDH), fp64 host algebra ------------------
+struct D3 {
+    double m[3][3];
+};
+
+D3 d3_eye()
+{
+    D3 r{};
+    for (int i = 0; i < 3; ++i) r.m[i][i] = 1.0;
+    return r;
+}
+
+D3 d3_mul(const D3& a, const D3& b)
+{
+    D3 r{};
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j)
+            for (int x = 0; x < 3; ++x) r.m[i][j] += a.m[i][x] * b.m[x][j];
+    return r;
+}
+
+// Rx / Ry / Rz of the reference (src/matrix_operations.cuh:136-161)
+D3 d3_rot(int axis, double t)
+{
+    D3 r = d3_eye();
+    const double c = cos(t), s = sin(t);
+    const int i = (axis + 1) % 3, j = (axis + 2) % 3;  // x: (y, z); y: (z, x); z: (x, y)
+    r.m[i][i] = c;
+    r.m[i][j] = -s;
+    r.m[j][i] = s;
+    r.m[j][j] = c;
+    return r;
+}
+
+// Q_c with Q_c Rz(t) Q_c^T = R_c(t): the cyclic permutation taking z to axis c.
+D3 d3_q(int c)
+{
+    D3 r{};
+    for (int i = 0; i < 3; ++i) r.m[(i + c + 1) % 3][i] = 1.0;  // Q e_i = e_{(i + c + 1) % 3}
+    return r;
+}
+
+D3 d3_t(const D3& a)
+{
+    D3 r{};
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) r.m[i][j] = a.m[j][i];
+    return r;
+}
 
 // Device record of one obj_t collider (ikpso_collide.h): the inverse
 // quaternion is quatInvert2's (same fp32 operations as the device would do)
@@ -197,6 +249,19 @@ ikpso_status parse_chain(const std::vector<ikpso_node>& nodes, const ikpso_pso_c
         }
     }
     ch.E = E;
+    // joint-axis mask: bit d = 3(k-1)+c of free_mask when Euler angle c of node k is free
+    ch.free_mask = 0;
+    for (int k = 1; k <= J; ++k)
+        for (int c = 0; c < 3; ++c) {
+            const int d = 3 * (k - 1) + c;
+            if (d >= 64) break;  // > 21 joints: no compiled kernel (rejected below)
+            if (!ex.axis_mask || ((ex.axis_mask[k] >> c) & 1)) ch.free_mask |= 1ull << d;
+        }
+    for (int k = 1; k <= J && ex.axis_mask; ++k)
+        if (ex.axis_mask[k] > 7) return IKPSO_ERR_INVALID_ARG;
+    ch.dfree = __builtin_popcountll(ch.free_mask);
+    ch.masked = 3 * J <= 64 && ch.dfree != 3 * J;
+    if (ch.dfree == 0) return IKPSO_ERR_INVALID_ARG;  // nothing to optimise
 #ifdef IKPSO_NO_UNIFORM_BOUNDS
     ch.uniform_bounds = false;
 #else
@@ -232,13 +297,114 @@ ikpso_status parse_chain(const std::vector<ikpso_node>& nodes, const ikpso_pso_c
     }
     if (ch.use_posref && ex.positions)
         for (int i = 0; i < 4 * J; ++i) ch.aux[i] = ex.positions[i + (ex.posref_node_slot ? 8 : 0)];
-    if (ch.use_penalty)
-        for (int d = 0; d < 3 * J; ++d) {
-            ch.aux[4 * J + d] = ex.soft_lo[d];
-            ch.aux[7 * J + d] = ex.soft_hi[d];
+    if (ch.use_penalty)  // soft limits are given per free dimension; a locked angle adds max(-inf, 0)^2 = 0
+        for (int d = 0, r = 0; d < 3 * J; ++d) {
+            const bool fr = d < 64 && ((ch.free_mask >> d) & 1);
+            ch.aux[4 * J + d] = fr ? ex.soft_lo[r] : -INFINITY;
+            ch.aux[7 * J + d] = fr ? ex.soft_hi[r] : INFINITY;
+            r += fr;
         }
     if (!chain_supported(ch)) return IKPSO_ERR_UNSUPPORTED;
     return IKPSO_OK;
+}
+
+// Number of compiled TopoDH instantiations (ikpso_inst_dh_*.hip).
+constexpr int kDHMin = 3, kDHMax = 12;
+
+// The folded form of a masked serial chain with a tip effector (TopoDH, FAST
+// kernels): every free Euler axis becomes one joint W_j = W_{j-1} C_j Rz(t_j),
+// q_j = q_{j-1} + W_j s_j (see TopoDH).  The constants are products of the
+// locked rotations (at their rest angles), the axis permutations Q_c, the
+// origin transform and the link translations, multiplied out in fp64 and
+// rounded once.  False when the chain does not fold (tree, several effectors,
+// distance or collider term, no compiled width).
+bool build_dh(const std::vector<ikpso_node>& nodes, const ChainHost& eu, const Extras& ex, ChainHost& dh)
+{
+    const int J = eu.J, N = eu.dfree;
+    if (eu.topo != TopoKind::SerialTip || eu.use_posref || eu.num_coll > 0 || !eu.masked) return false;
+    if (N < kDHMin || N > kDHMax) return false;
+    const ikpso_node& o = nodes[0];
+    D3 g = d3_mul(d3_mul(d3_rot(0, o.rotation[0]), d3_rot(1, o.rotation[1])), d3_rot(2, o.rotation[2]));
+    double sc[3] = {o.position[0], o.position[1], o.position[2]};  // offset in the current joint frame
+    std::vector<D3> C;
+    std::vector<std::array<double, 3>> S;
+    std::array<double, 3> q0{};
+    for (int k = 1; k <= J; ++k) {
+        for (int c = 0; c < 3; ++c) {
+            const int d = 3 * (k - 1) + c;
+            if ((eu.free_mask >> d) & 1) {
+                if (C.empty())
+                    q0 = {sc[0], sc[1], sc[2]};
+                else
+                    S.back() = {sc[0], sc[1], sc[2]};
+                C.push_back(d3_mul(g, d3_q(c)));
+                S.push_back({0.0, 0.0, 0.0});
+                g = d3_t(d3_q(c));
+                sc[0] = sc[1] = sc[2] = 0.0;
+            } else {
+                g = d3_mul(g, d3_rot(c, nodes[k].rotation[c]));
+            }
+        }
+        const double len = nodes[k].length;  // T(len, 0, 0) after the node's rotation
+        for (int r = 0; r < 3; ++r) sc[r] += len * g.m[r][0];
+    }
+    S.back() = {sc[0], sc[1], sc[2]};
+    dh = ChainHost{};
+    dh.J = N;
+    dh.E = 1;
+    dh.topo = TopoKind::DH;
+    dh.parent.assign(N + 1, -1);
+    dh.eff_slot.assign(N + 1, -1);
+    dh.len.assign(N + 1, 0.0f);
+    dh.eff_w.assign(N + 1, 0.0f);
+    dh.lo.assign(3 * N, 0.0f);
+    dh.hi.assign(3 * N, 0.0f);
+    dh.rest.assign(3 * N, 0.0f);
+    dh.tgt0.assign(3 * N, 0.0f);
+    for (int k = 1; k <= N; ++k) dh.parent[k] = k - 1;
+    dh.eff_slot[N] = 0;
+    dh.eff_w[N] = eu.eff_w[J];
+    for (int c = 0; c < 3; ++c) dh.tgt0[3 * (N - 1) + c] = eu.tgt0[3 * (J - 1) + c];
+    for (int d = 0, r = 0; d < 3 * J; ++d)
+        if ((eu.free_mask >> d) & 1) {
+            dh.lo[r] = eu.lo[d];
+            dh.hi[r] = eu.hi[d];
+            dh.rest[r] = eu.rest[d];
+            ++r;
+        }
+    dh.uniform_bounds = true;
+    for (int d = 0; d < N; ++d)
+        dh.uniform_bounds = dh.uniform_bounds && as_bits(dh.lo[d]) == as_bits(dh.lo[0]) &&
+                            as_bits(dh.hi[d]) == as_bits(dh.hi[0]);
+    dh.w = eu.w;
+    dh.c1 = eu.c1;
+    dh.c2 = eu.c2;
+    dh.aw_j = eu.aw_j;  // angleWeight / node count of the chain, as calculateDistance
+    dh.dw_j = 0.0f;
+    dh.use_posref = false;
+    dh.lim_w = eu.lim_w;
+    dh.use_penalty = eu.use_penalty;
+    dh.coll_off = ((size_t)10 * N + 15) & ~size_t(15);
+    dh.dh_off = dh.coll_off;
+    dh.aux.assign(dh.dh_off + 12 * (size_t)N + 4, 0.0f);
+    if (dh.use_penalty)
+        for (int d = 0, r = 0; d < 3 * J; ++d)
+            if ((eu.free_mask >> d) & 1) {
+                dh.aux[4 * N + r] = ex.soft_lo[r];
+                dh.aux[7 * N + r] = ex.soft_hi[r];
+                ++r;
+            }
+    dh.free_mask = (1ull << N) - 1;
+    dh.dfree = N;
+    dh.masked = false;
+    float* dc = dh.aux.data() + dh.dh_off;
+    for (int j = 0; j < N; ++j) {
+        for (int r = 0; r < 3; ++r)
+            for (int c = 0; c < 3; ++c) dc[12 * j + 3 * r + c] = (float)C[j].m[r][c];
+        for (int r = 0; r < 3; ++r) dc[12 * j + 9 + r] = (float)S[j][r];
+    }
+    for (int r = 0; r < 3; ++r) dc[12 * N + r] = (float)q0[r];
+    return chain_supported(dh);
 }
 
 // Device scratch of the reference-compatible path (result staging, aux terms,
@@ -379,8 +545,14 @@ int pick_kernel(const ChainHost& ch, int mode, int P, int requested)
 }  // namespace
 
 struct ikpso_solver {
-    ChainHost chain;
+    ChainHost chain;       // the node table as given (Euler form, with its axis mask)
     float* aux = nullptr;  // device copy of chain.aux
+    // The folded form (TopoDH) a FAST solver of a masked serial chain solves with;
+    // evaluate and REFERENCE solves use `chain`.
+    ChainHost dhchain;
+    bool use_dh = false;
+    float* aux_dh = nullptr;
+    const ChainHost& solve_chain() const { return use_dh ? dhchain : chain; }
     int family = IKPSO_KERNEL_RESIDENT;
     int requested = IKPSO_KERNEL_AUTO;
     std::string kname;     // kernel family / topology, for ikpso_solver_kernel_name
@@ -432,7 +604,8 @@ ikpso_status solve_streaming(ikpso_solver* s, void** ws, size_t* ws_bytes, const
                              const float* start_pose, int64_t num_swarms, int32_t iterations, float* out_angles,
                              float* out_fitness, float* out_residual, hipStream_t hs)
 {
-    const int D = 3 * s->chain.J;
+    const ChainHost& ch = s->solve_chain();
+    const int D = ch.kernel_dims();
     ikpso_status st = grow(ws, ws_bytes, stream_workspace_bytes(num_swarms, s->P, D, true));
     if (st != IKPSO_OK) return st;
     StreamIO io{};
@@ -443,7 +616,7 @@ ikpso_status solve_streaming(ikpso_solver* s, void** ws, size_t* ws_bytes, const
     io.out_angles = out_angles;
     io.out_fitness = out_fitness;
     io.out_residual = out_residual;
-    IKPSO_HIP(launch_stream(s->chain, s->mode, io, iterations, hs));
+    IKPSO_HIP(launch_stream(ch, s->mode, io, iterations, hs));
     return IKPSO_OK;
 }
 
@@ -614,12 +787,21 @@ ikpso_status ikpso_solver_create(const ikpso_solver_desc* desc, ikpso_solver** o
         return IKPSO_ERR_INVALID_ARG;
     if (desc->arith != IKPSO_ARITH_FAST && desc->arith != IKPSO_ARITH_REFERENCE) return IKPSO_ERR_INVALID_ARG;
     *out = nullptr;
-    const int J = desc->node_count - 1, D = 3 * J;
+    const int J = desc->node_count - 1;
     std::vector<ikpso_node> nodes(desc->node_count);
     ikpso_status st = fetch_any(nodes.data(), desc->chain, sizeof(ikpso_node) * desc->node_count);
     if (st != IKPSO_OK) return st;
     std::vector<float> pos, slo, shi;
+    std::vector<uint8_t> mask;
     Extras ex;
+    int D = 3 * J;  // free dimensions
+    if (desc->axis_mask) {
+        mask.resize(desc->node_count);
+        if ((st = fetch_any(mask.data(), desc->axis_mask, mask.size())) != IKPSO_OK) return st;
+        ex.axis_mask = mask.data();
+        D = 0;
+        for (int k = 1; k <= J; ++k) D += __builtin_popcount(mask[k] & 7u);
+    }
     if (desc->fit.distance_weight != 0.0f && desc->positions) {
         ex.posref_node_slot = (desc->flags & IKPSO_FLAG_POSREF_NODE_SLOT) != 0;
         const size_t n = 4 * (size_t)(ex.posref_node_slot ? J + 2 : J);
@@ -655,23 +837,35 @@ ikpso_status ikpso_solver_create(const ikpso_solver_desc* desc, ikpso_solver** o
     }
     s->P = desc->particles;
     s->mode = desc->arith;
+    // FAST solves of a masked serial chain run on its folded form
+    s->use_dh = s->mode == IKPSO_ARITH_FAST && !(desc->flags & IKPSO_FLAG_NO_FOLD) &&
+                build_dh(nodes, s->chain, ex, s->dhchain);
     {
         const size_t bytes = sizeof(float) * s->chain.aux.size();
         hipError_t e = hipMalloc(&s->aux, bytes);
         if (e == hipSuccess) e = hipMemcpy(s->aux, s->chain.aux.data(), bytes, hipMemcpyHostToDevice);
+        if (e == hipSuccess && s->use_dh) {
+            const size_t b2 = sizeof(float) * s->dhchain.aux.size();
+            e = hipMalloc(&s->aux_dh, b2);
+            if (e == hipSuccess) e = hipMemcpy(s->aux_dh, s->dhchain.aux.data(), b2, hipMemcpyHostToDevice);
+        }
         if (e != hipSuccess) {
             if (s->aux) (void)hipFree(s->aux);
+            if (s->aux_dh) (void)hipFree(s->aux_dh);
             delete s;
             return hip_status(e);
         }
         s->chain.aux_dev = s->aux;
+        s->dhchain.aux_dev = s->aux_dh;
     }
-    s->family = pick_kernel(s->chain, s->mode, s->P, desc->kernel);
+    const ChainHost& sch = s->solve_chain();
+    s->family = pick_kernel(sch, s->mode, s->P, desc->kernel);
     s->requested = desc->kernel;
-    if (s->family >= 0) s->kname = kernel_name(s->chain, s->family);
-    if (s->family >= 0) s->kname_latency = kernel_name(s->chain, IKPSO_KERNEL_COOP) + " (latency variant)";
+    if (s->family >= 0) s->kname = kernel_name(sch, s->family);
+    if (s->family >= 0) s->kname_latency = kernel_name(sch, IKPSO_KERNEL_COOP) + " (latency variant)";
     if (s->family < 0 || desc->kernel < IKPSO_KERNEL_AUTO || desc->kernel > IKPSO_KERNEL_COOP) {
         (void)hipFree(s->aux);
+        if (s->aux_dh) (void)hipFree(s->aux_dh);
         delete s;
         return (desc->kernel == IKPSO_KERNEL_RESIDENT || desc->kernel == IKPSO_KERNEL_COOP) ? IKPSO_ERR_UNSUPPORTED
                                                                                               : IKPSO_ERR_INVALID_ARG;
@@ -687,6 +881,7 @@ ikpso_status ikpso_solver_destroy(ikpso_solver* s)
     if (s->rng_snap) (void)hipFree(s->rng_snap);
     if (s->ws_fallback) (void)hipFree(s->ws_fallback);
     if (s->aux) (void)hipFree(s->aux);
+    if (s->aux_dh) (void)hipFree(s->aux_dh);
     if (s->ws) (void)hipFree(s->ws);
     delete s;
     return IKPSO_OK;
@@ -722,8 +917,9 @@ ikpso_status ikpso_solve_batch(ikpso_solver* s, const float* targets, const floa
         const ikpso_status st = ikpso_solver_sync(s);
         if (st != IKPSO_OK) return st;
     }
+    const ChainHost& ch = s->solve_chain();
     const bool latency_coop = s->family == IKPSO_KERNEL_RESIDENT && s->requested == IKPSO_KERNEL_AUTO &&
-                              prefer_latency_coop(s->chain, s->mode, s->P, num_swarms);
+                              prefer_latency_coop(ch, s->mode, s->P, num_swarms);
     s->last_latency = latency_coop;
     if (s->family == IKPSO_KERNEL_RESIDENT && !latency_coop) {
         SwarmIO io{};
@@ -736,13 +932,13 @@ ikpso_status ikpso_solve_batch(ikpso_solver* s, const float* targets, const floa
         io.P = s->P;
         io.iterations = iterations;
         io.num_swarms = num_swarms;
-        IKPSO_HIP(launch_resident(s->chain, s->mode, io, hs));
+        IKPSO_HIP(launch_resident(ch, s->mode, io, hs));
         return IKPSO_OK;
     }
-    const int D = 3 * s->chain.J;
+    const int D = ch.kernel_dims();
     if (s->family == IKPSO_KERNEL_COOP || latency_coop) {
         int G, NG, T;
-        if (!coop_plan(s->chain, s->mode, s->P, num_swarms, s->requested == IKPSO_KERNEL_AUTO, &G, &NG, &T))
+        if (!coop_plan(ch, s->mode, s->P, num_swarms, s->requested == IKPSO_KERNEL_AUTO, &G, &NG, &T))
             return IKPSO_ERR_UNSUPPORTED;
         ikpso_status st = grow(&s->ws, &s->ws_bytes, coop_workspace_bytes(NG, G, D));
         if (st != IKPSO_OK) return st;
@@ -768,7 +964,7 @@ ikpso_status ikpso_solve_batch(ikpso_solver* s, const float* targets, const floa
         io.iterations = iterations;
         io.num_swarms = num_swarms;
         IKPSO_HIP(carve_coop(io, s->ws, G, NG, T, D, hs));
-        IKPSO_HIP(launch_coop(s->chain, s->mode, io, hs));
+        IKPSO_HIP(launch_coop(ch, s->mode, io, hs));
         s->pending.active = true;
         s->pending.targets = targets;
         s->pending.start_pose = start_pose;
@@ -822,7 +1018,7 @@ ikpso_status ikpso_solver_evaluate(ikpso_solver* s, const float* angles, const f
     return IKPSO_OK;
 }
 
-int ikpso_solver_dof(const ikpso_solver* s) { return s ? 3 * s->chain.J : 0; }
+int ikpso_solver_dof(const ikpso_solver* s) { return s ? s->chain.dof() : 0; }
 int ikpso_solver_effectors(const ikpso_solver* s) { return s ? s->chain.E : 0; }
 const char* ikpso_solver_kernel_name(const ikpso_solver* s)
 {

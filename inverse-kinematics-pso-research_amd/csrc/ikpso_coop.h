@@ -72,15 +72,15 @@ struct CoopShared {
 // chunks, reduce; returns the group-wide minimum key of this exchange (uniform)
 // and leaves the winner's local best in sh.g when it improves on `gkey` (or
 // always when `force`).  Called by every wave; wave 0 does the global work.
-template <int J, int BLOCK>
-__device__ __forceinline__ void coop_exchange(SwarmShared<J>& sh, CoopShared<J>& cs, const float* s_pb,
+template <class Topo, int BLOCK>
+__device__ __forceinline__ void coop_exchange(SwarmShared<Topo>& sh, CoopShared<Topo::J>& cs, const float* s_pb,
                                               uint32_t local_key, int32_t* error, uint32_t spin_limit, bool force)
 {
-    constexpr int D = 3 * J;
+    constexpr int D = Topo::D;
     constexpr int SLOT = kCoopSlot(D);
     static_assert(D + 2 <= 64, "wave 0 publishes the record in one store instruction");
     int lidx;
-    const uint32_t lmin = swarm_argmin<J>(sh, 0, local_key, &lidx);  // one workgroup barrier inside
+    const uint32_t lmin = swarm_argmin(sh, 0, local_key, &lidx);  // one workgroup barrier inside
     if (wave_id() == 0) {
         compiler_fence();
         const int G = cs.G, member = cs.member;
@@ -100,13 +100,16 @@ __device__ __forceinline__ void coop_exchange(SwarmShared<J>& sh, CoopShared<J>&
         if (lane == 0) {
             __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             uint32_t n = 0;
-            while (ld_sc1(counter) < target) {
-                if (n++ >= spin_limit) {
-                    timed_out = 1;
-                    break;
+            if (spin_limit == 0)  // debug knob (IKPSO_COOP_SPIN_LIMIT=0): always take the give-up path
+                timed_out = 1;
+            else
+                while (ld_sc1(counter) < target) {
+                    if (n++ >= spin_limit) {
+                        timed_out = 1;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(2);
                 }
-                __builtin_amdgcn_s_sleep(2);
-            }
         }
         timed_out = __builtin_amdgcn_readfirstlane(timed_out);  // lane 0's verdict
         asm volatile("" ::: "memory");
@@ -130,18 +133,18 @@ __device__ __forceinline__ void coop_exchange(SwarmShared<J>& sh, CoopShared<J>&
     __syncthreads();
 }
 
-// BLOCK: kCoopThreads<J>() (throughput: fill each CU), or kCoopLatencyThreads
+// BLOCK: kCoopThreads<D>() (throughput: fill each CU), or kCoopLatencyThreads
 // for a few swarms (latency: one wave per SIMD on 4x more CUs).
 template <class Topo, int MODE, int TERMS, int BLOCK>
 __global__ void __launch_bounds__(BLOCK, (BLOCK >= 256 ? BLOCK / 256 : 1))
     k_swarm_coop(const ChainConsts<Topo::J> cc, const SwarmIO io)
 {
     constexpr int J = Topo::J;
-    constexpr int D = 3 * J;
+    constexpr int D = Topo::D;
     const int tid = threadIdx.x;
     const int P = io.P;
 
-    __shared__ SwarmShared<J> sh;
+    __shared__ SwarmShared<Topo> sh;
     __shared__ CoopShared<J> cs;
     // local bests [d][lane]; padded to > 80 KiB so a CU never holds two
     // workgroups (the launch geometry assumes one per CU)
@@ -168,7 +171,7 @@ __global__ void __launch_bounds__(BLOCK, (BLOCK >= 256 ? BLOCK / 256 : 1))
         const int64_t b = cs.b;
         if (b >= io.num_swarms) break;
         const int i = cs.member * BLOCK + tid;  // particle index within the swarm
-        stage_swarm_inputs<J>(cc, io.targets, io.start_pose, b, sh);
+        stage_swarm_inputs<Topo>(cc, io.targets, io.start_pose, b, sh);
         // the add-for-shift issue form only in the latency variant (one wave per
         // SIMD, room to spare): in the 2-wave serial-20 kernel it cost 5 %
         using Rng = XorwowT<(BLOCK == kCoopLatencyThreads) && std::is_same_v<RngFor<TERMS>, XorwowT<true>>>;
@@ -179,22 +182,17 @@ __global__ void __launch_bounds__(BLOCK, (BLOCK >= 256 ? BLOCK / 256 : 1))
 
         // initParticlesKernel + initLocalBests (src/kernel.cu:191-266)
         float x[D], v[D];
-#pragma unroll
-        for (int d = 0; d < D; ++d) {
-            x[d] = sh.rest[d];
-            v[d] = __builtin_fmaf(rng.uniform(), 2.0f, -1.0f);
-            s_pb[d * BLOCK + tid] = x[d];
-        }
-        float pbf = fitness<Topo, MODE, TERMS>(cc, x, sh.rest, sh.tgt, nullptr);
+        init_particle<Topo, TERMS, BLOCK>(cc, sh, s_pb, tid, x, v, rng);
+        float pbf = fitness<Topo, MODE, TERMS>(cc, x, sh.rest, sh.tgt, nullptr, sh.dh);
         // swarm argmin + unconditional first global-best copy (src/kernel.cu:297-304)
-        coop_exchange<J, BLOCK>(sh, cs, s_pb, i < P ? ordered_key(pbf) : 0xFFFFFFFFu, io.coop_error, io.coop_spin_limit, true);
+        coop_exchange<Topo, BLOCK>(sh, cs, s_pb, i < P ? ordered_key(pbf) : 0xFFFFFFFFu, io.coop_error, io.coop_spin_limit, true);
 
         for (int it = 0; it < io.iterations; ++it) {
             compiler_fence();
             if (cs.abort) break;
             swarm_step<Topo, MODE, TERMS, BLOCK>(cc, sh, s_pb, tid, x, v, pbf, coef, rng);
             const bool act = cs.member * BLOCK + tid < P;
-            coop_exchange<J, BLOCK>(sh, cs, s_pb, act ? ordered_key(pbf) : 0xFFFFFFFFu, io.coop_error, io.coop_spin_limit, false);
+            coop_exchange<Topo, BLOCK>(sh, cs, s_pb, act ? ordered_key(pbf) : 0xFFFFFFFFu, io.coop_error, io.coop_spin_limit, false);
         }
 
         compiler_fence();
@@ -202,13 +200,13 @@ __global__ void __launch_bounds__(BLOCK, (BLOCK >= 256 ? BLOCK / 256 : 1))
         const int64_t bb = cs.b;
         const int ii = member * BLOCK + tid;
         if (member == 0) {  // outputs (updateGlobalBestCoordsKernel) + fitness + residual
-            if (tid < D) io.out_angles[bb * D + tid] = sh.g[tid];
+            store_angles<Topo>(cc, io.out_angles, bb, tid, tid < D ? sh.g[tid] : 0.0f);
             if (tid == 0 && io.out_fitness) io.out_fitness[bb] = key_to_float(cs.gkey);
             if (io.out_residual && tid < 64) {
                 float g[D];
 #pragma unroll
                 for (int d = 0; d < D; ++d) g[d] = sh.g[d];
-                const float r = residual<Topo, MODE>(cc, g, sh.tgt);
+                const float r = residual<Topo, MODE, TERMS>(cc, g, sh.tgt, sh.dh);
                 if (tid == 0) io.out_residual[bb] = r;
             }
         }
@@ -229,7 +227,7 @@ __global__ void __launch_bounds__(BLOCK, (BLOCK >= 256 ? BLOCK / 256 : 1))
         if (cs.abort) {     // a wait timed out: mark this and every later swarm of the group as failed
             if (member == 0)
                 for (int64_t r = bb; r < io.num_swarms; r += io.coop_ng) {
-                    if (tid < D) io.out_angles[r * D + tid] = __builtin_nanf("");
+                    if (tid < cc.dfree) io.out_angles[r * cc.dfree + tid] = __builtin_nanf("");
                     if (tid == 0 && io.out_fitness) io.out_fitness[r] = __builtin_nanf("");
                     if (tid == 0 && io.out_residual) io.out_residual[r] = __builtin_nanf("");
                 }
@@ -262,27 +260,30 @@ inline hipError_t launch_coop_block(const ChainConsts<Topo::J>& cc, const SwarmI
 template <class Topo, int MODE, int TERMS>
 inline hipError_t launch_coop_kernel(const ChainConsts<Topo::J>& cc, const SwarmIO& io, hipStream_t stream)
 {
-    if constexpr (kCoopThreads<Topo::J>() != kCoopLatencyThreads) {
+    if constexpr (kCoopThreads<Topo::D>() != kCoopLatencyThreads) {
         if (io.coop_block == kCoopLatencyThreads)
             return launch_coop_block<Topo, MODE, TERMS, kCoopLatencyThreads>(cc, io, stream);
     }
-    if (io.coop_block != kCoopThreads<Topo::J>()) return hipErrorInvalidValue;
-    return launch_coop_block<Topo, MODE, TERMS, kCoopThreads<Topo::J>()>(cc, io, stream);
+    if (io.coop_block != kCoopThreads<Topo::D>()) return hipErrorInvalidValue;
+    return launch_coop_block<Topo, MODE, TERMS, kCoopThreads<Topo::D>()>(cc, io, stream);
 }
 
 template <class Topo, int MODE>
 inline hipError_t run_coop(const ChainHost& ch, const SwarmIO& io, hipStream_t stream)
 {
     const ChainConsts<Topo::J> cc = make_consts<Topo::J>(ch);
-    const int terms = (ch.use_posref ? kTermPosRef : 0) | (ch.use_penalty ? kTermPenalty : 0) |
-                      (ch.uniform_bounds ? kTermUniformBounds : 0) | (ch.num_coll > 0 ? kTermColliders : 0);
-    if constexpr (!Topo::kGeneric && MODE == IKPSO_ARITH_FAST) {
+    const int terms = term_set(ch);
+    hipError_t err = hipSuccess;
+    if (dh_terms<Topo>(terms, &err,
+                       [&](auto t) { return launch_coop_kernel<Topo, MODE, decltype(t)::value>(cc, io, stream); }))
+        return err;
+    if constexpr (!Topo::kGeneric && !Topo::kDH && MODE == IKPSO_ARITH_FAST) {
         if (terms == kTermUniformBounds) return launch_coop_kernel<Topo, MODE, kTermUniformBounds>(cc, io, stream);
         if (terms == (kTermUniformBounds | kTermPenalty))
             return launch_coop_kernel<Topo, MODE, kTermUniformBounds | kTermPenalty>(cc, io, stream);
     }
-    if (ch.num_coll > 0) return launch_coop_kernel<Topo, MODE, kTermRuntime | kTermColliders>(cc, io, stream);
-    return launch_coop_kernel<Topo, MODE, kTermRuntime>(cc, io, stream);
+    return with_runtime_terms<Topo>(
+        ch, [&](auto t) { return launch_coop_kernel<Topo, MODE, decltype(t)::value>(cc, io, stream); });
 }
 
 }  // namespace ikpso

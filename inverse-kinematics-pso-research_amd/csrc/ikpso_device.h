@@ -13,6 +13,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "ikpso_collide.h"
 #include "ikpso_params.h"
 
@@ -40,6 +42,13 @@
 #ifndef IKPSO_ISSUE_SHL1_ADD
 #define IKPSO_ISSUE_SHL1_ADD 1
 #endif
+// FAST-mode sin/cos on the transcendental unit (v_sin_f32 / v_cos_f32) in the
+// kernels that run 4 waves per SIMD (chains of <= 10 joints) and have no
+// collider term; see sincos_fast.
+#ifndef IKPSO_SINCOS_HW
+#define IKPSO_SINCOS_HW 1
+#endif
+
 
 namespace ikpso {
 
@@ -161,12 +170,29 @@ __host__ __device__ inline void xorwow_seed(uint64_t seed, uint32_t st[6])
 // flips.  Measured on gfx950 against correctly rounded sin/cos over 2^26
 // arguments in [-100, 100]: max 1 ulp, 71-73% correctly rounded
 // (tools/probes/trig_probe.hip).
+// HW: the transcendental unit instead (below).
+template <bool HW = false>
 __host__ __device__ __forceinline__ void sincos_fast(float x, float* s_out, float* c_out)
 {
 #if IKPSO_ABL_NOSIN  // timing-only ablation
     *s_out = x * 0.5f;
     *c_out = __builtin_fmaf(-0.5f, x, 1.0f);
     return;
+#endif
+#if defined(__HIP_DEVICE_COMPILE__)
+    if constexpr (HW) {
+        // v_sin_f32 / v_cos_f32 on x / 2pi (revolutions; the transcendental unit
+        // reduces its own argument).  tools/probes/trig_probe.hip on gfx950: max
+        // abs error 4.8e-7 on [0, 2pi] and 2.7e-7 on [-pi, pi] (vs 6e-8 for the
+        // polynomial); 8 cycles per wave64 op each (tools/probes/valu_probe.hip),
+        // 3 instructions per angle against ~20 for the polynomial: -7 % kernel
+        // time on the reference scene.  With 2 waves per SIMD (long chains) the
+        // transcendental latency is exposed and the polynomial is faster (+13 %).
+        const float rev = x * 0.159154943091895336f;
+        *s_out = __builtin_amdgcn_sinf(rev);
+        *c_out = __builtin_amdgcn_cosf(rev);
+        return;
+    }
 #endif
 #if IKPSO_SINCOS_V2
     // Quadrant by the round-to-integer magic constant: k_big = x*2/pi + 1.5*2^23
@@ -252,9 +278,11 @@ __host__ __device__ __forceinline__ void sincos_reference(float x, float* s_out,
 
 // The reference's scene (src/Main.cpp:76-116): origin -> 4 elbows -> 3 wrist
 // effectors hanging off the last elbow; DFS parent indices [-1,0,1,2,3,4,4,4].
+//   A: angles per node (3 Euler angles; 1 for the folded chain), D = A*J the
+//   kernel's dimensions; kDH: the folded serial chain (FitnessAccDH).
 struct TopoRef7 {
-    static constexpr int J = 7;
-    static constexpr bool kGeneric = false;
+    static constexpr int J = 7, A = 3, D = 21;
+    static constexpr bool kGeneric = false, kDH = false;
     __host__ __device__ static constexpr int parent(int k) { return k <= 5 ? k - 1 : 4; }
     __host__ __device__ static constexpr bool leaf(int k) { return k >= 5; }  // no child reads its frame
     __host__ __device__ static constexpr bool effector(int k) { return k >= 5; }
@@ -263,8 +291,8 @@ struct TopoRef7 {
 // Serial chain of J joints with one tip effector (BASELINE config 5: J = 20).
 template <int J_>
 struct TopoSerialTip {
-    static constexpr int J = J_;
-    static constexpr bool kGeneric = false;
+    static constexpr int J = J_, A = 3, D = 3 * J_;
+    static constexpr bool kGeneric = false, kDH = false;
     __host__ __device__ static constexpr int parent(int k) { return k - 1; }
     __host__ __device__ static constexpr bool leaf(int k) { return k == J_; }
     __host__ __device__ static constexpr bool effector(int k) { return k == J_; }
@@ -274,12 +302,45 @@ struct TopoSerialTip {
 // every node weighted by its effector weight (0 for non-effectors).
 template <int J_>
 struct TopoGeneric {
-    static constexpr int J = J_;
-    static constexpr bool kGeneric = true;
+    static constexpr int J = J_, A = 3, D = 3 * J_;
+    static constexpr bool kGeneric = true, kDH = false;
     __host__ __device__ static constexpr int parent(int k) { return k - 1; }  // unused
     __host__ __device__ static constexpr bool leaf(int) { return false; }
     __host__ __device__ static constexpr bool effector(int) { return true; }
 };
+
+// A serial chain with a tip effector whose free angles are folded into J
+// single-axis joints (extension, SURVEY.md §8(f) row 4: joint-axis mask / DH
+// arms): every free Euler axis c of node k is written R_c(t) = Q_c Rz(t) Q_c^T,
+// and every constant factor between two free axes -- the locked Euler angles,
+// the Q_c, whole locked nodes, the origin transform -- is multiplied out on the
+// host (fp64) into C_j, and every link length into the offset s_j:
+//   W_j = W_{j-1} C_j Rz(t_j),   q_j = q_{j-1} + W_j s_j,   tip = q_J.
+// One sincos per free angle and no work for locked ones (the Euler form pays 3
+// sincos per node and, with locked axes emulated by equal clamp bounds, draws
+// and updates for every dead dimension).  FAST arithmetic only: REFERENCE runs
+// use the Euler kernels with the mask, which keep the reference's operation
+// order.  J = number of free angles = D.
+template <int J_>
+struct TopoDH {
+    static constexpr int J = J_, A = 1, D = J_;
+    static constexpr bool kGeneric = false, kDH = true;
+    __host__ __device__ static constexpr int parent(int k) { return k - 1; }
+    __host__ __device__ static constexpr bool leaf(int k) { return k == J_; }
+    __host__ __device__ static constexpr bool effector(int k) { return k == J_; }
+};
+
+// Free-dimension helpers (ChainConsts::free_mask, identity without a mask).
+template <class CC>
+__device__ __forceinline__ bool dim_free(const CC& cc, int d)
+{
+    return (cc.free_mask >> d) & 1;
+}
+template <class CC>
+__device__ __forceinline__ int dim_rank(const CC& cc, int d)  // index among the free dimensions
+{
+    return __builtin_popcountll(cc.free_mask & ((1ull << d) - 1));
+}
 
 // ------------------------------------------------------------------ frames
 // World transform of one node: rotation R (row-major 3x3) and position p.
@@ -300,12 +361,13 @@ __device__ __forceinline__ Frame origin_frame(const float* m0)
 // FAST: closed-form local rotation Rx(a)Ry(b)Rz(c), then world = parent * local,
 // FMA contraction allowed.  For leaf nodes only the position is consumed and
 // the compiler drops the unused rotation entries.
+template <bool HW>
 __device__ __forceinline__ Frame child_frame_fast(const Frame& P, float a, float b, float c, float len)
 {
     float sa, ca, sb, cb, sc, cc;
-    sincos_fast(a, &sa, &ca);
-    sincos_fast(b, &sb, &cb);
-    sincos_fast(c, &sc, &cc);
+    sincos_fast<HW>(a, &sa, &ca);
+    sincos_fast<HW>(b, &sb, &cb);
+    sincos_fast<HW>(c, &sc, &cc);
     const float p = sa * sb, q = ca * sb;
     const float l00 = cb * cc, l01 = -cb * sc, l02 = sb;
     const float l10 = p * cc + ca * sc, l11 = ca * cc - p * sc, l12 = -sa * cb;
@@ -331,12 +393,13 @@ __device__ __forceinline__ Frame child_frame_fast(const Frame& P, float a, float
 // of two columns (12 multiply-adds), 36 in all against 14 + 27 for building
 // the local matrix and multiplying it in.  Leaves, which only need the first
 // column, keep the closed form (the compiler then drops the other columns).
+template <bool HW>
 __device__ __forceinline__ Frame child_frame_fast_seq(const Frame& P, float a, float b, float c, float len)
 {
     float sa, ca, sb, cb, sc, cc;
-    sincos_fast(a, &sa, &ca);
-    sincos_fast(b, &sb, &cb);
-    sincos_fast(c, &sc, &cc);
+    sincos_fast<HW>(a, &sa, &ca);
+    sincos_fast<HW>(b, &sb, &cb);
+    sincos_fast<HW>(c, &sc, &cc);
     // * Rx(a): columns 1, 2 become (ca c1 + sa c2, ca c2 - sa c1)
     const float x01 = P.r01 * ca + P.r02 * sa, x02 = P.r02 * ca - P.r01 * sa;
     const float x11 = P.r11 * ca + P.r12 * sa, x12 = P.r12 * ca - P.r11 * sa;
@@ -406,16 +469,16 @@ __device__ __forceinline__ Frame child_frame_reference(const Frame& P, float a, 
 }
 
 // SEQ: FAST mode may compose the rotation column-wise (interior nodes, or any
-// node whose full frame is consumed).
-template <int MODE, bool SEQ = false>
+// node whose full frame is consumed).  HW: FAST sin/cos on the transcendental unit.
+template <int MODE, bool SEQ = false, bool HW = false>
 __device__ __forceinline__ Frame child_frame(const Frame& P, float a, float b, float c, float len)
 {
     if constexpr (MODE == IKPSO_ARITH_REFERENCE)
         return child_frame_reference(P, a, b, c, len);
     else if constexpr (SEQ && IKPSO_FK_SEQ)
-        return child_frame_fast_seq(P, a, b, c, len);
+        return child_frame_fast_seq<HW>(P, a, b, c, len);
     else
-        return child_frame_fast(P, a, b, c, len);
+        return child_frame_fast<HW>(P, a, b, c, len);
 }
 
 // ---------------------------------------------------------------- fitness
@@ -434,13 +497,28 @@ __device__ __forceinline__ Frame child_frame(const Frame& P, float a, float b, f
 // instead of per dimension from LDS.
 // kTermColliders: the collider (GJK) block of calculateDistance
 // (src/kernel.cu:104-136), compiled in only when the scene has colliders.
-constexpr int kTermPosRef = 1, kTermPenalty = 2, kTermRuntime = 4, kTermUniformBounds = 8, kTermColliders = 16;
+// kTermMask: the chain has a joint-axis mask (ChainConsts::free_mask): locked
+// angles take no draws and no update (uniform branches per dimension, which
+// cost the register allocator enough that unmasked chains get builds without).
+constexpr int kTermPosRef = 1, kTermPenalty = 2, kTermRuntime = 4, kTermUniformBounds = 8, kTermColliders = 16,
+              kTermMask = 32;
 
 // Generator type of a swarm kernel: the add-for-shift issue form everywhere but
 // in the collider kernels, whose register allocation the opaque add perturbs
 // (spills); the draws are bit-identical either way.
 template <int TERMS>
 using RngFor = XorwowT<IKPSO_ISSUE_SHL1_ADD != 0 && !(TERMS & kTermColliders)>;
+
+// FAST sin/cos on the transcendental unit (sincos_fast<true>) for a kernel of
+// this topology and term set: chains that run 4 waves per SIMD, no collider term
+// (whose contact decisions the tests compare across kernels bit for bit).
+template <class Topo, int MODE, int TERMS>
+constexpr bool kHwTrig = IKPSO_SINCOS_HW && MODE == IKPSO_ARITH_FAST && !(TERMS & kTermColliders) && Topo::D <= 30;
+
+// Which kernel builds honour ChainConsts::free_mask (the host routes masked
+// chains to them; the folded chain has no locked angles).
+template <class Topo, int TERMS>
+constexpr bool kMasked = (TERMS & kTermMask) && !Topo::kDH;
 
 
 template <class Topo, int MODE, int TERMS>
@@ -450,7 +528,7 @@ struct FitnessAcc {
     float rot_diff, pos_diff, distance, pen;
     bool hit, posref, penalty;
 
-    __device__ __forceinline__ explicit FitnessAcc(const ChainConsts<J>& cc)
+    __device__ __forceinline__ explicit FitnessAcc(const ChainConsts<J>& cc, const float* = nullptr)
         : rot_diff(0.0f), pos_diff(0.0f), distance(0.0f), pen(0.0f), hit(false),
           posref((TERMS & kTermPosRef) || ((TERMS & kTermRuntime) && cc.use_posref)),
           penalty((TERMS & kTermPenalty) || ((TERMS & kTermRuntime) && cc.use_penalty))
@@ -466,10 +544,11 @@ struct FitnessAcc {
 #pragma clang fp contract(off)
         const int pk = Topo::kGeneric ? cc.parent[k] : Topo::parent(k);
         // column-wise composition unless only the leaf's position is consumed
+        constexpr bool HW = kHwTrig<Topo, MODE, TERMS>;
         if (!Topo::kGeneric && (!Topo::leaf(k) || (TERMS & kTermColliders)))
-            F[k] = child_frame<MODE, true>(F[pk], a, b, c, cc.len[k]);
+            F[k] = child_frame<MODE, true, HW>(F[pk], a, b, c, cc.len[k]);
         else
-            F[k] = child_frame<MODE>(F[pk], a, b, c, cc.len[k]);
+            F[k] = child_frame<MODE, false, HW>(F[pk], a, b, c, cc.len[k]);
         const float dx = rest3[0] - a, dy = rest3[1] - b, dz = rest3[2] - c;
         if constexpr (MODE == IKPSO_ARITH_REFERENCE) {
             rot_diff = rot_diff + ((dx * dx + dy * dy) + dz * dz);
@@ -521,6 +600,13 @@ struct FitnessAcc {
         }
     }
 
+    // The same with the node's angles, rest angles and target by pointer.
+    __device__ __forceinline__ void node(const ChainConsts<J>& cc, int k, const float* ang, const float* rest3,
+                                         const float* tgt3, float* node_pos)
+    {
+        node(cc, k, ang[0], ang[1], ang[2], rest3, tgt3, node_pos);
+    }
+
     __device__ __forceinline__ float finish(const ChainConsts<J>& cc) const
     {
 #pragma clang fp contract(off)
@@ -531,15 +617,126 @@ struct FitnessAcc {
     }
 };
 
+// FK + fitness of the folded serial chain (TopoDH; FAST arithmetic): the tip
+// effector term, the angle term over the free angles and the soft-limit
+// penalty -- calculateDistance (src/kernel.cu:64-151) of the chain with its
+// locked angles at rest (the locked angles add exact zeros to the angle term).
+// No distance or collider term (the host routes those chains to the Euler
+// kernels).  `dhc` = the folded chain's constants (12 floats per joint + q0;
+// ChainConsts::dh_off): the swarm kernels' LDS copy, passed unconditionally so
+// the loads stay ds_read (a pointer that may be LDS or global is a flat pointer,
+// and flat loads of LDS data cost vector-memory latency).
+template <class Topo, int MODE, int TERMS>
+struct FitnessAccDH {
+    static constexpr int J = Topo::J;
+    static constexpr bool HW = kHwTrig<Topo, MODE, TERMS>;
+    static_assert(MODE == IKPSO_ARITH_FAST, "the folded chain is FAST arithmetic only");
+    const float* dhc;
+    float w00, w01, w02, w10, w11, w12, w20, w21, w22;  // current joint frame W_j
+    float qx, qy, qz;                                   // position q_j
+    float px, py, pz;                                   // tip (after joint J)
+    float rot_diff, distance, pen;
+    bool penalty;
+
+    __device__ __forceinline__ FitnessAccDH(const ChainConsts<J>& cc, const float* dh)
+        : dhc(dh), rot_diff(0.0f), distance(0.0f), pen(0.0f),
+          penalty((TERMS & kTermPenalty) || ((TERMS & kTermRuntime) && cc.use_penalty))
+    {
+        qx = dhc[12 * J + 0];
+        qy = dhc[12 * J + 1];
+        qz = dhc[12 * J + 2];
+    }
+
+    // Joint k (1..J) at angle t: W = W * C_k * Rz(t), then q += W s_k.
+    __device__ __forceinline__ void advance(int k, float t)
+    {
+        float st, ct;
+        sincos_fast<HW>(t, &st, &ct);
+        const float* C = dhc + 12 * (k - 1);
+        float m00, m01, m02, m10, m11, m12, m20, m21, m22;
+        if (k == 1) {
+            m00 = C[0]; m01 = C[1]; m02 = C[2];
+            m10 = C[3]; m11 = C[4]; m12 = C[5];
+            m20 = C[6]; m21 = C[7]; m22 = C[8];
+        } else {
+            const float c00 = C[0], c01 = C[1], c02 = C[2], c10 = C[3], c11 = C[4], c12 = C[5], c20 = C[6],
+                        c21 = C[7], c22 = C[8];
+            m00 = w00 * c00 + w01 * c10 + w02 * c20;
+            m01 = w00 * c01 + w01 * c11 + w02 * c21;
+            m02 = w00 * c02 + w01 * c12 + w02 * c22;
+            m10 = w10 * c00 + w11 * c10 + w12 * c20;
+            m11 = w10 * c01 + w11 * c11 + w12 * c21;
+            m12 = w10 * c02 + w11 * c12 + w12 * c22;
+            m20 = w20 * c00 + w21 * c10 + w22 * c20;
+            m21 = w20 * c01 + w21 * c11 + w22 * c21;
+            m22 = w20 * c02 + w21 * c12 + w22 * c22;
+        }
+        const float s0 = C[9], s1 = C[10], s2 = C[11];
+        if (k == J) {
+            // the tip only needs W s = M (Rz(t) s)
+            const float v0 = ct * s0 - st * s1, v1 = st * s0 + ct * s1;
+            px = qx + m00 * v0 + m01 * v1 + m02 * s2;
+            py = qy + m10 * v0 + m11 * v1 + m12 * s2;
+            pz = qz + m20 * v0 + m21 * v1 + m22 * s2;
+        } else {
+            // * Rz(t): columns 0, 1 become (ct c0 + st c1, ct c1 - st c0)
+            w00 = ct * m00 + st * m01; w01 = ct * m01 - st * m00; w02 = m02;
+            w10 = ct * m10 + st * m11; w11 = ct * m11 - st * m10; w12 = m12;
+            w20 = ct * m20 + st * m21; w21 = ct * m21 - st * m20; w22 = m22;
+            qx = qx + w00 * s0 + w01 * s1 + w02 * s2;
+            qy = qy + w10 * s0 + w11 * s1 + w12 * s2;
+            qz = qz + w20 * s0 + w21 * s1 + w22 * s2;
+        }
+    }
+
+    // Joint k with its one angle, rest angle and (tip) target.
+    __device__ __forceinline__ void node(const ChainConsts<J>& cc, int k, const float* ang, const float* rest,
+                                         const float* tgt3, float* node_pos)
+    {
+        const float t = ang[0];
+        advance(k, t);
+        const float dt = rest[0] - t;
+        rot_diff = rot_diff + dt * dt;
+        if (penalty) {
+            const int d = k - 1;
+            const float slo = cc.aux[4 * J + d], shi = cc.aux[7 * J + d];
+            const float over = fmaxf(fmaxf(t - shi, slo - t), 0.0f);
+            pen = pen + over * over;
+        }
+        if (k == J) {
+            const float ex = px - tgt3[0], ey = py - tgt3[1], ez = pz - tgt3[2];
+            distance = ((ex * ex + ey * ey) + ez * ez) * cc.eff_w[J];
+            if (node_pos) {  // [3J]: the tip's slot
+                node_pos[3 * (J - 1) + 0] = px;
+                node_pos[3 * (J - 1) + 1] = py;
+                node_pos[3 * (J - 1) + 2] = pz;
+            }
+        }
+    }
+
+    __device__ __forceinline__ float finish(const ChainConsts<J>& cc) const
+    {
+        float f = distance + cc.aw_j * rot_diff;
+        if (penalty) f = f + cc.lim_w * pen;
+        return f;
+    }
+};
+
+template <class Topo, int MODE, int TERMS>
+using FitnessFor =
+    std::conditional_t<Topo::kDH, FitnessAccDH<Topo, MODE, TERMS>, FitnessAcc<Topo, MODE, TERMS>>;
+
+// x, rest: [D]; tgt: [3J] (per node); dhc: the folded chain's constants (TopoDH).
 template <class Topo, int MODE, int TERMS>
 __device__ __forceinline__ float fitness(const ChainConsts<Topo::J>& cc, const float* x, const float* rest,
-                                         const float* tgt, float* node_pos /* [3J] or nullptr */)
+                                         const float* tgt, float* node_pos /* [3J] or nullptr */,
+                                         const float* dhc = nullptr)
 {
-    FitnessAcc<Topo, MODE, TERMS> acc(cc);
+    constexpr int A = Topo::A;
+    FitnessFor<Topo, MODE, TERMS> acc(cc, dhc);
 #pragma unroll
     for (int k = 1; k <= Topo::J; ++k) {
-        acc.node(cc, k, x[3 * (k - 1) + 0], x[3 * (k - 1) + 1], x[3 * (k - 1) + 2], rest + 3 * (k - 1),
-                 tgt + 3 * (k - 1), node_pos);
+        acc.node(cc, k, x + A * (k - 1), rest + A * (k - 1), tgt + 3 * (k - 1), node_pos);
 #if IKPSO_SCHED_NODE
         // One node at a time: keeps the scheduler from hoisting all 3J
         // independent sincos evaluations to the top of the evaluation.
@@ -550,26 +747,39 @@ __device__ __forceinline__ float fitness(const ChainConsts<Topo::J>& cc, const f
 }
 
 // Sum over effectors of the Euclidean distance to target (checkDistance,
-// src/Main.cpp:290-298 / src/Node.h:421-429), evaluated with the device FK.
-template <class Topo, int MODE>
-__device__ __forceinline__ float residual(const ChainConsts<Topo::J>& cc, const float* x, const float* tgt)
+// src/Main.cpp:290-298 / src/Node.h:421-429), evaluated with the device FK
+// (TERMS: the calling kernel's, for its sin/cos flavour).
+template <class Topo, int MODE, int TERMS>
+__device__ __forceinline__ float residual(const ChainConsts<Topo::J>& cc, const float* x, const float* tgt,
+                                          const float* dhc = nullptr)
 {
     constexpr int J = Topo::J;
-    Frame F[J + 1];
-    F[0] = origin_frame(cc.m0);
-    float r = 0.0f;
+    if constexpr (Topo::kDH) {
+        FitnessAccDH<Topo, MODE, TERMS> acc(cc, dhc);
 #pragma unroll
-    for (int k = 1; k <= J; ++k) {
-        const int pk = Topo::kGeneric ? cc.parent[k] : Topo::parent(k);
-        F[k] = child_frame<MODE>(F[pk], x[3 * (k - 1)], x[3 * (k - 1) + 1], x[3 * (k - 1) + 2], cc.len[k]);
-        if (Topo::effector(k) && cc.eff_slot[k] >= 0) {
-            const float dx = tgt[3 * (k - 1) + 0] - F[k].px;
-            const float dy = tgt[3 * (k - 1) + 1] - F[k].py;
-            const float dz = tgt[3 * (k - 1) + 2] - F[k].pz;
-            r += sqrtf(dx * dx + dy * dy + dz * dz);
+        for (int k = 1; k <= J; ++k) acc.advance(k, x[k - 1]);
+        const float dx = tgt[3 * (J - 1) + 0] - acc.px;
+        const float dy = tgt[3 * (J - 1) + 1] - acc.py;
+        const float dz = tgt[3 * (J - 1) + 2] - acc.pz;
+        return sqrtf(dx * dx + dy * dy + dz * dz);
+    } else {
+        Frame F[J + 1];
+        F[0] = origin_frame(cc.m0);
+        float r = 0.0f;
+#pragma unroll
+        for (int k = 1; k <= J; ++k) {
+            const int pk = Topo::kGeneric ? cc.parent[k] : Topo::parent(k);
+            F[k] = child_frame<MODE, false, kHwTrig<Topo, MODE, TERMS>>(F[pk], x[3 * (k - 1)], x[3 * (k - 1) + 1],
+                                                                        x[3 * (k - 1) + 2], cc.len[k]);
+            if (Topo::effector(k) && cc.eff_slot[k] >= 0) {
+                const float dx = tgt[3 * (k - 1) + 0] - F[k].px;
+                const float dy = tgt[3 * (k - 1) + 1] - F[k].py;
+                const float dz = tgt[3 * (k - 1) + 2] - F[k].pz;
+                r += sqrtf(dx * dx + dy * dy + dz * dz);
+            }
         }
+        return r;
     }
-    return r;
 }
 
 // ------------------------------------------------------------ PSO update

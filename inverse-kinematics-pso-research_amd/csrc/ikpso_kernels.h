@@ -32,7 +32,9 @@ namespace ikpso {
 
 // Ref7: the reference scene's tree with effectors on nodes 5..7; SerialTip:
 // serial chain with a single tip effector; Generic: anything else.
-enum class TopoKind { Ref7, SerialTip, Generic };
+// DH: a serial chain with a tip effector folded into its free angles (TopoDH;
+// built from a masked chain by the API layer, FAST arithmetic).
+enum class TopoKind { Ref7, SerialTip, Generic, DH };
 
 // The chain as the kernels need it, parsed once from the caller's node table.
 struct ChainHost {
@@ -41,7 +43,7 @@ struct ChainHost {
     TopoKind topo = TopoKind::Generic;
     std::vector<int> parent, eff_slot;
     std::vector<float> len, eff_w, lo, hi, rest, tgt0;
-    // [posref 4J | soft_lo 3J | soft_hi 3J | collider records 16*num_coll] (host copy)
+    // [posref 4J | soft_lo 3J | soft_hi 3J | collider records 16*num_coll | TopoDH constants] (host copy)
     std::vector<float> aux;
     const float* aux_dev = nullptr;  // device copy, owned by the solver / call
     float m0[12] = {};
@@ -50,6 +52,14 @@ struct ChainHost {
     bool uniform_bounds = false;  // every angle has clamp bounds lo[0], hi[0]
     int num_coll = 0;             // colliders (obj_t) of the scene
     size_t coll_off = 0;          // float offset of the collider records in aux
+    // joint-axis mask over the kernel's dimensions (all set: no mask) and the
+    // number of free dimensions, which is the API's D
+    uint64_t free_mask = 0;
+    int dfree = 0;
+    bool masked = false;          // some Euler angle is locked: runtime-term kernels only
+    size_t dh_off = 0;            // TopoDH constants in aux (ChainConsts::dh_off), 12 J + 4 floats
+    int dof() const { return dfree; }
+    int kernel_dims() const { return topo == TopoKind::DH ? J : 3 * J; }
 };
 
 // Evaluate-kernel parameters.
@@ -62,22 +72,23 @@ struct EvalIO {
     int64_t n;
 };
 
-// Threads per workgroup the resident kernel is compiled for: 1024 lanes
-// (16 waves, 4 per SIMD, <= 128 VGPRs) while x/v/pbest of one particle fit,
-// 256 lanes (one wave per SIMD, up to 512 VGPRs) for long chains.
-template <int J>
+// Threads per workgroup the resident kernel is compiled for, by the kernel's
+// dimension count D: 1024 lanes (16 waves, 4 per SIMD, <= 128 VGPRs) while
+// x/v/pbest of one particle fit (D <= 30), 256 lanes (one wave per SIMD, up to
+// 512 VGPRs) for long chains.
+template <int D>
 __host__ __device__ constexpr int kResidentMaxThreads()
 {
-    return J <= 10 ? 1024 : 256;
+    return D <= 30 ? 1024 : 256;
 }
 
 // Threads per workgroup of the cooperative kernel: the resident kernel's 1024
 // for short chains; 512 (2 waves per SIMD, <= 256 VGPRs, 120 KiB of local bests
 // at D = 60) for long ones.  One workgroup per CU either way (LDS).
-template <int J>
+template <int D>
 __host__ __device__ constexpr int kCoopThreads()
 {
-    return J <= 10 ? 1024 : 512;
+    return D <= 30 ? 1024 : 512;
 }
 
 // Published record of one chunk: key, global particle index, D floats, padded
@@ -131,6 +142,9 @@ ChainConsts<J> make_consts(const ChainHost& h)
     c.num_eff = h.E;
     c.num_coll = h.num_coll;
     c.coll = h.num_coll && h.aux_dev ? reinterpret_cast<const CollRec*>(h.aux_dev + h.coll_off) : nullptr;
+    c.free_mask = h.free_mask;
+    c.dfree = h.dfree;
+    c.dh_off = (int32_t)h.dh_off;
     return c;
 }
 

@@ -61,7 +61,7 @@ hipError_t launch_init_generators(ikpso_rng_state* st, int64_t count, uint64_t s
 int resident_max_threads(const ChainHost& ch)
 {
     int r = 0;
-    visit_topology(ch, [&](auto topo) { r = kResidentMaxThreads<decltype(topo)::J>(); });
+    visit_topology(ch, [&](auto topo) { r = kResidentMaxThreads<decltype(topo)::D>(); });
     return r;
 }
 
@@ -80,6 +80,8 @@ std::string kernel_name(const ChainHost& ch, int family)
         using T = decltype(t);
         if constexpr (std::is_same_v<T, TopoRef7>)
             topo = "ref_tree7";
+        else if constexpr (T::kDH)
+            topo = "dh" + std::to_string(T::J);
         else if constexpr (!T::kGeneric)
             topo = "serial_tip" + std::to_string(T::J);
     });
@@ -120,7 +122,7 @@ hipError_t launch_coop(const ChainHost& ch, int mode, const SwarmIO& io, hipStre
     hipError_t err = hipErrorInvalidValue;
     const bool ok = visit_topology(ch, [&](auto topo) {
         using T = decltype(topo);
-        if (io.coop_g * kCoopThreads<T::J>() < io.P || io.coop_g > 64) return;  // G chunks must cover the swarm
+        if (io.coop_g * kCoopThreads<T::D>() < io.P || io.coop_g > 64) return;  // G chunks must cover the swarm
         err = TopoOps<T>::coop(ch, mode, io, stream);
     });
     return ok ? err : hipErrorInvalidValue;
@@ -135,8 +137,8 @@ bool coop_geometry(const ChainHost& ch, int mode, CoopGeometry* g)
     visit_topology(ch, [&](auto topo) {
         using T = decltype(topo);
         if constexpr (!T::kGeneric) {
-            g->threads = kCoopThreads<T::J>();
-            g->latency_variant = kCoopThreads<T::J>() != kCoopLatencyThreads;
+            g->threads = kCoopThreads<T::D>();
+            g->latency_variant = kCoopThreads<T::D>() != kCoopLatencyThreads;
             spec = true;
         }
     });

@@ -35,6 +35,20 @@ struct ChainConsts {
     int32_t num_eff;
     int32_t num_coll;         // colliders (kTermColliders kernels only)
     const struct CollRec* coll;  // [num_coll] device records, inside the aux buffer
+    // Joint-axis mask (extension): bit d set when kernel
+    // dimension d is a PSO dimension; dfree = popcount.  The kernels of the
+    // Euler topologies run over all 3J Euler angles and honour the mask in their
+    // runtime-term builds (locked angles stay at rest: no draws, no update, no
+    // clamp); the API's angle vectors carry the dfree free dimensions only.
+    uint64_t free_mask;
+    int32_t dfree;
+    // Folded serial chain (TopoDH): aux + dh_off holds, per joint j = 1..J, the
+    // constant rotation C_j (row-major 3x3) between the previous joint frame and
+    // this joint's Rz and the constant offset s_j (3) travelled in this joint's
+    // frame; then the base position q0 (3).  A device array rather than kernarg
+    // fields: the kernels stage it in LDS with a runtime-indexed loop, which on a
+    // by-value kernarg struct costs a private copy of the whole struct.
+    int32_t dh_off;
 };
 
 // Per-launch buffers.

@@ -19,6 +19,10 @@
 #include "ikpso_kernels.h"
 #include "ikpso_swarm.h"
 
+#ifndef IKPSO_DH_NODE_BARRIER
+#define IKPSO_DH_NODE_BARRIER 0
+#endif
+
 namespace ikpso {
 
 // One PSO iteration of one particle (lane `tid`) of a swarm whose local bests
@@ -31,54 +35,60 @@ namespace ikpso {
 // reference's update-all-then-evaluate values in the same order.  The
 // node's LDS operands (local best, global best, rest pose, target) are
 // loaded one node ahead so their latency hides under the previous node.
+// Masked chains (kMasked builds): a locked dimension takes no draws and keeps
+// its rest value, as in the oracle's masked restatement.
 template <class Topo, int MODE, int TERMS, int BLOCK, class Rng>
-__device__ __forceinline__ void swarm_step(const ChainConsts<Topo::J>& cc, SwarmShared<Topo::J>& sh, float* s_pb,
-                                           int tid, float (&x)[3 * Topo::J], float (&v)[3 * Topo::J], float& pbf,
+__device__ __forceinline__ void swarm_step(const ChainConsts<Topo::J>& cc, SwarmShared<Topo>& sh, float* s_pb,
+                                           int tid, float (&x)[Topo::D], float (&v)[Topo::D], float& pbf,
                                            const PsoCoef& coef, Rng& rng)
 {
-    constexpr int J = Topo::J;
-    constexpr int D = 3 * J;
-    FitnessAcc<Topo, MODE, TERMS> acc(cc);
-    float npb[3], ng[3], nrest[3], ntgt[3];
+    constexpr int J = Topo::J, A = Topo::A, D = Topo::D;
+    constexpr bool MASK = kMasked<Topo, TERMS>;
+    FitnessFor<Topo, MODE, TERMS> acc(cc, sh.dh);
+    float npb[A], ng[A], nrest[A], ntgt[3];
 #pragma unroll
-    for (int ax = 0; ax < 3; ++ax) {
+    for (int ax = 0; ax < A; ++ax) {
         npb[ax] = s_pb[ax * BLOCK + tid];
         ng[ax] = sh.g[ax];
         nrest[ax] = sh.rest[ax];
-        ntgt[ax] = Topo::effector(1) ? sh.tgt[ax] : 0.0f;
     }
 #pragma unroll
-    for (int k = 1; k <= J; ++k) {
-        float cpb[3], cg[3], crest[3], ctgt[3];
+    for (int c = 0; c < 3; ++c) ntgt[c] = Topo::effector(1) ? sh.tgt[c] : 0.0f;
 #pragma unroll
-        for (int ax = 0; ax < 3; ++ax) {
+    for (int k = 1; k <= J; ++k) {
+        float cpb[A], cg[A], crest[A], ctgt[3];
+#pragma unroll
+        for (int ax = 0; ax < A; ++ax) {
             cpb[ax] = npb[ax];
             cg[ax] = ng[ax];
             crest[ax] = nrest[ax];
-            ctgt[ax] = ntgt[ax];
         }
+#pragma unroll
+        for (int c = 0; c < 3; ++c) ctgt[c] = ntgt[c];
         if (k < J) {
 #pragma unroll
-            for (int ax = 0; ax < 3; ++ax) {
-                const int d = 3 * k + ax;
+            for (int ax = 0; ax < A; ++ax) {
+                const int d = A * k + ax;
                 npb[ax] = s_pb[d * BLOCK + tid];
                 ng[ax] = sh.g[d];
                 nrest[ax] = sh.rest[d];
-                ntgt[ax] = Topo::effector(k + 1) ? sh.tgt[d] : 0.0f;
             }
+#pragma unroll
+            for (int c = 0; c < 3; ++c) ntgt[c] = Topo::effector(k + 1) ? sh.tgt[3 * k + c] : 0.0f;
         }
 #pragma unroll
-        for (int ax = 0; ax < 3; ++ax) {
-            const int d = 3 * (k - 1) + ax;
+        for (int ax = 0; ax < A; ++ax) {
+            const int d = A * (k - 1) + ax;
+            if (MASK && !dim_free(cc, d)) continue;  // locked: stays at rest
             pso_update<MODE>(x[d], v[d], cpb[ax], cg[ax], coef, rng);
             if constexpr (TERMS & kTermUniformBounds)
                 x[d] = clamp_mode<MODE>(x[d], cc.lo[0], cc.hi[0]);
             else
                 x[d] = clamp_mode<MODE>(x[d], sh.lo[d], sh.hi[d]);
         }
-        acc.node(cc, k, x[3 * (k - 1)], x[3 * (k - 1) + 1], x[3 * (k - 1) + 2], crest, ctgt, nullptr);
+        acc.node(cc, k, x + A * (k - 1), crest, ctgt, nullptr);
 #if !IKPSO_RES_NO_NODE_BARRIER
-        __builtin_amdgcn_sched_barrier(0);
+        if (!Topo::kDH || IKPSO_DH_NODE_BARRIER) __builtin_amdgcn_sched_barrier(0);
 #endif
     }
 
@@ -91,45 +101,57 @@ __device__ __forceinline__ void swarm_step(const ChainConsts<Topo::J>& cc, Swarm
     }
 }
 
+// initParticlesKernel (src/kernel.cu:223-266) for one particle: warm start at
+// the current pose, v = U*2-1 (one draw per free dimension, in dimension
+// order), local best = x.
+template <class Topo, int TERMS, int BLOCK, class Rng>
+__device__ __forceinline__ void init_particle(const ChainConsts<Topo::J>& cc, const SwarmShared<Topo>& sh,
+                                              float* s_pb, int tid, float (&x)[Topo::D], float (&v)[Topo::D],
+                                              Rng& rng)
+{
+#pragma unroll
+    for (int d = 0; d < Topo::D; ++d) {
+        x[d] = sh.rest[d];
+        if (kMasked<Topo, TERMS> && !dim_free(cc, d))
+            v[d] = 0.0f;
+        else
+            v[d] = __builtin_fmaf(rng.uniform(), 2.0f, -1.0f);
+        s_pb[d * BLOCK + tid] = x[d];
+    }
+}
+
 // ------------------------------------------------------- resident swarm kernel
 template <class Topo, int MODE, int TERMS>
-__global__ void __launch_bounds__(kResidentMaxThreads<Topo::J>())
+__global__ void __launch_bounds__(kResidentMaxThreads<Topo::D>())
     k_swarm_resident(const ChainConsts<Topo::J> cc, const SwarmIO io)
 {
-    constexpr int J = Topo::J;
-    constexpr int D = 3 * J;
-    constexpr int BLOCK = kResidentMaxThreads<J>();
+    constexpr int D = Topo::D;
+    constexpr int BLOCK = kResidentMaxThreads<D>();
     const int64_t b = blockIdx.x;
     const int tid = threadIdx.x;
     const int P = io.P;
     const bool active = tid < P;
 
-    __shared__ SwarmShared<J> sh;
+    __shared__ SwarmShared<Topo> sh;
     // Local-best positions, [d][lane]: read once per iteration by the update,
     // written on improvement; consecutive lanes hit consecutive banks.
     __shared__ float s_pb[D * BLOCK];
-    stage_swarm_inputs<J>(cc, io.targets, io.start_pose, b, sh);
+    stage_swarm_inputs<Topo>(cc, io.targets, io.start_pose, b, sh);
 
     RngFor<TERMS> rng{0, 0, 0, 0, 0, 0};
     if (active) load_rng(rng, io.rng + b * P + tid);
     __syncthreads();
 
-    // initParticlesKernel (src/kernel.cu:223-266): warm start at the current
-    // pose, v = U*2-1 (D draws in dimension order), pbest = x.
+    // initParticlesKernel (src/kernel.cu:223-266)
     float x[D], v[D];
-#pragma unroll
-    for (int d = 0; d < D; ++d) {
-        x[d] = sh.rest[d];
-        v[d] = __builtin_fmaf(rng.uniform(), 2.0f, -1.0f);
-        s_pb[d * BLOCK + tid] = x[d];
-    }
+    init_particle<Topo, TERMS, BLOCK>(cc, sh, s_pb, tid, x, v, rng);
     // initLocalBests (src/kernel.cu:191-200)
-    float pbf = fitness<Topo, MODE, TERMS>(cc, x, sh.rest, sh.tgt, nullptr);
+    float pbf = fitness<Topo, MODE, TERMS>(cc, x, sh.rest, sh.tgt, nullptr, sh.dh);
 
     // swarm argmin + unconditional first global-best copy (src/kernel.cu:297-304)
     int bidx;
-    uint32_t gkey = swarm_argmin<J>(sh, 0, active ? ordered_key(pbf) : 0xFFFFFFFFu, &bidx);
-    copy_gbest<J, BLOCK>(sh, s_pb, bidx);
+    uint32_t gkey = swarm_argmin(sh, 0, active ? ordered_key(pbf) : 0xFFFFFFFFu, &bidx);
+    copy_gbest<Topo, BLOCK>(sh, s_pb, bidx);
     __syncthreads();
 
     const PsoCoef coef = pso_coef(cc);
@@ -142,24 +164,24 @@ __global__ void __launch_bounds__(kResidentMaxThreads<Topo::J>())
         const uint32_t bmin = gkey;
         asm volatile("" ::"v"(pbf));
 #else
-        const uint32_t bmin = swarm_argmin<J>(sh, (it + 1) & 1, active ? ordered_key(pbf) : 0xFFFFFFFFu, &bidx);
+        const uint32_t bmin = swarm_argmin(sh, (it + 1) & 1, active ? ordered_key(pbf) : 0xFFFFFFFFu, &bidx);
 #endif
         if (bmin < gkey) {  // uniform across the workgroup
             gkey = bmin;
-            copy_gbest<J, BLOCK>(sh, s_pb, bidx);
+            copy_gbest<Topo, BLOCK>(sh, s_pb, bidx);
             __syncthreads();
         }
     }
 
     // outputs: Coordinates result (updateGlobalBestCoordsKernel) + fitness + residual
     compiler_fence();
-    if (tid < D) io.out_angles[b * D + tid] = sh.g[tid];
+    store_angles<Topo>(cc, io.out_angles, b, tid, tid < D ? sh.g[tid] : 0.0f);
     if (tid == 0 && io.out_fitness) io.out_fitness[b] = key_to_float(gkey);
     if (io.out_residual && tid < 64) {
         float g[D];
 #pragma unroll
         for (int d = 0; d < D; ++d) g[d] = sh.g[d];
-        const float r = residual<Topo, MODE>(cc, g, sh.tgt);
+        const float r = residual<Topo, MODE, TERMS>(cc, g, sh.tgt, sh.dh);
         if (tid == 0) io.out_residual[b] = r;
     }
     if (active) {
@@ -178,18 +200,22 @@ __global__ void __launch_bounds__(kResidentMaxThreads<Topo::J>())
 }
 
 // ----------------------------------------------------------- evaluate kernel
+// angles, rest: [n][dfree] over the free dimensions (locked ones at the chain's rest).
 template <class Topo, int MODE, int TERMS>
 __global__ void __launch_bounds__(256) k_evaluate(const ChainConsts<Topo::J> cc, EvalIO io)
 {
     constexpr int J = Topo::J;
-    constexpr int D = 3 * J;
+    constexpr int D = Topo::D;
+    const int64_t DF = cc.dfree;
     for (int64_t n = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; n < io.n;
          n += (int64_t)gridDim.x * blockDim.x) {
-        float x[D], rest[D], tgt[D], pos[D];
+        float x[D], rest[D], tgt[3 * J], pos[3 * J];
 #pragma unroll
         for (int d = 0; d < D; ++d) {
-            x[d] = io.angles[n * D + d];
-            rest[d] = io.rest ? io.rest[n * D + d] : cc.rest[d];
+            const bool fr = dim_free(cc, d);
+            const int64_t r = n * DF + dim_rank(cc, d);
+            x[d] = fr ? io.angles[r] : cc.rest[d];
+            rest[d] = io.rest && fr ? io.rest[r] : cc.rest[d];
         }
         if (io.targets) {
 #pragma unroll
@@ -201,13 +227,13 @@ __global__ void __launch_bounds__(256) k_evaluate(const ChainConsts<Topo::J> cc,
             }
         } else {
 #pragma unroll
-            for (int d = 0; d < D; ++d) tgt[d] = cc.tgt0[d];
+            for (int d = 0; d < 3 * J; ++d) tgt[d] = cc.tgt0[d];
         }
         const float f = fitness<Topo, MODE, TERMS>(cc, x, rest, tgt, pos);
         if (io.out_fitness) io.out_fitness[n] = f;
         if (io.out_positions) {
 #pragma unroll
-            for (int d = 0; d < D; ++d) io.out_positions[n * D + d] = pos[d];
+            for (int d = 0; d < 3 * J; ++d) io.out_positions[n * 3 * J + d] = pos[d];
         }
     }
 }
@@ -224,9 +250,14 @@ inline hipError_t run_resident(const ChainHost& ch, const SwarmIO& io, int block
     // kernels; everything else (generic topologies, the distance term, every
     // REFERENCE-mode run) tests the terms at run time with the same arithmetic,
     // with the collider block compiled in only when the scene has colliders.
-    const int terms = (ch.use_posref ? kTermPosRef : 0) | (ch.use_penalty ? kTermPenalty : 0) |
-                      (ch.uniform_bounds ? kTermUniformBounds : 0) | (ch.num_coll > 0 ? kTermColliders : 0);
-    if constexpr (!Topo::kGeneric && MODE == IKPSO_ARITH_FAST) {
+    const int terms = term_set(ch);
+    hipError_t err = hipSuccess;
+    if (dh_terms<Topo>(terms, &err, [&](auto t) {
+            hipLaunchKernelGGL((k_swarm_resident<Topo, MODE, decltype(t)::value>), grid, threads, 0, stream, cc, io);
+            return hipGetLastError();
+        }))
+        return err;
+    if constexpr (!Topo::kGeneric && !Topo::kDH && MODE == IKPSO_ARITH_FAST) {
         if (terms == kTermUniformBounds) {
             hipLaunchKernelGGL((k_swarm_resident<Topo, MODE, kTermUniformBounds>), grid, threads, 0, stream, cc, io);
             return hipGetLastError();
@@ -238,21 +269,23 @@ inline hipError_t run_resident(const ChainHost& ch, const SwarmIO& io, int block
         }
     }
     (void)terms;
-    if (ch.num_coll > 0)
-        hipLaunchKernelGGL((k_swarm_resident<Topo, MODE, kTermRuntime | kTermColliders>), grid, threads, 0, stream, cc,
-                           io);
-    else
-        hipLaunchKernelGGL((k_swarm_resident<Topo, MODE, kTermRuntime>), grid, threads, 0, stream, cc, io);
-    return hipGetLastError();
+    return with_runtime_terms<Topo>(ch, [&](auto t) {
+        hipLaunchKernelGGL((k_swarm_resident<Topo, MODE, decltype(t)::value>), grid, threads, 0, stream, cc, io);
+        return hipGetLastError();
+    });
 }
 
 template <class Topo, int MODE>
 inline hipError_t run_evaluate(const ChainHost& ch, const EvalIO& io, hipStream_t stream)
 {
+    if constexpr (Topo::kDH) {  // the solver evaluates through its Euler chain
+        return hipErrorNotSupported;
+    } else {
     const ChainConsts<Topo::J> cc = make_consts<Topo::J>(ch);
     int64_t blocks = (io.n + 255) / 256;
     if (blocks > 8192) blocks = 8192;
     if (blocks < 1) blocks = 1;
+    // the mask only places the given angles (no PSO): the unmasked builds evaluate it
     if (ch.num_coll > 0)
         hipLaunchKernelGGL((k_evaluate<Topo, MODE, kTermRuntime | kTermColliders>), dim3((unsigned)blocks), dim3(256),
                            0, stream, cc, io);
@@ -260,6 +293,7 @@ inline hipError_t run_evaluate(const ChainHost& ch, const EvalIO& io, hipStream_
         hipLaunchKernelGGL((k_evaluate<Topo, MODE, kTermRuntime>), dim3((unsigned)blocks), dim3(256), 0, stream, cc,
                            io);
     return hipGetLastError();
+    }
 }
 
 }  // namespace ikpso

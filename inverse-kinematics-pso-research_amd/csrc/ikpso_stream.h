@@ -32,10 +32,10 @@ namespace ikpso {
 // chunk partials of slot (t-1)&1, compare with the global best of slot
 // (t-1)&1, stage the resulting vector in sh.g.  Uniform across the workgroup.
 // Workgroup 0 of each swarm publishes the result to slot t&1.
-template <int J>
-__device__ __forceinline__ uint32_t stream_resolve_gbest(const StreamIO& io, int64_t b, int c, SwarmShared<J>& sh)
+template <class Topo>
+__device__ __forceinline__ uint32_t stream_resolve_gbest(const StreamIO& io, int64_t b, int c, SwarmShared<Topo>& sh)
 {
-    constexpr int D = 3 * J;
+    constexpr int D = Topo::D;
     const int lane = threadIdx.x & 63;
     const int prev = (io.t - 1) & 1, cur = io.t & 1;
     const int64_t B = io.num_swarms;
@@ -68,13 +68,13 @@ __device__ __forceinline__ uint32_t stream_resolve_gbest(const StreamIO& io, int
 
 // Chunk argmin of the local-best keys -> partial slot t&1; the winner lane
 // publishes its pbest vector (its own stores of this launch, read back).
-template <int J>
-__device__ __forceinline__ void stream_publish_chunk(const StreamIO& io, int64_t b, int c, SwarmShared<J>& sh,
+template <class Topo>
+__device__ __forceinline__ void stream_publish_chunk(const StreamIO& io, int64_t b, int c, SwarmShared<Topo>& sh,
                                                      uint32_t key, const Planes& pl)
 {
-    constexpr int D = 3 * J;
+    constexpr int D = Topo::D;
     int widx;
-    const uint32_t m = swarm_argmin<J>(sh, 0, key, &widx);
+    const uint32_t m = swarm_argmin(sh, 0, key, &widx);
     const int cur = io.t & 1;
     const int64_t slot = ((int64_t)cur * io.num_swarms + b) * io.C + c;
     if (threadIdx.x == 0) {
@@ -91,15 +91,14 @@ __device__ __forceinline__ void stream_publish_chunk(const StreamIO& io, int64_t
 template <class Topo, int MODE, int TERMS>
 __global__ void __launch_bounds__(kStreamChunk) k_stream_init(const ChainConsts<Topo::J> cc, const StreamIO io)
 {
-    constexpr int J = Topo::J;
-    constexpr int D = 3 * J;
+    constexpr int D = Topo::D;
     const int64_t b = blockIdx.x / io.C;
     const int c = blockIdx.x % io.C;
     const int i = c * kStreamChunk + threadIdx.x;
     const bool active = i < io.P;
     const int64_t P = io.P;
-    __shared__ SwarmShared<J> sh;
-    stage_swarm_inputs<J>(cc, io.targets, io.start_pose, b, sh);
+    __shared__ SwarmShared<Topo> sh;
+    stage_swarm_inputs<Topo>(cc, io.targets, io.start_pose, b, sh);
     __syncthreads();
 
     const Planes pl(io.state + b * 3 * D * P, D, (int)P, i);
@@ -113,10 +112,13 @@ __global__ void __launch_bounds__(kStreamChunk) k_stream_init(const ChainConsts<
         for (int d = 0; d < D; ++d) {
             x[d] = sh.rest[d];
             pl.st(0, d, x[d]);
-            pl.st(1, d, __builtin_fmaf(rng.uniform(), 2.0f, -1.0f));
+            if (kMasked<Topo, TERMS> && !dim_free(cc, d))  // locked: no draw
+                pl.st(1, d, 0.0f);
+            else
+                pl.st(1, d, __builtin_fmaf(rng.uniform(), 2.0f, -1.0f));
             pl.st(2, d, x[d]);
         }
-        pbf = fitness<Topo, MODE, TERMS>(cc, x, sh.rest, sh.tgt, nullptr);
+        pbf = fitness<Topo, MODE, TERMS>(cc, x, sh.rest, sh.tgt, nullptr, sh.dh);
         io.pbf[b * P + i] = pbf;
         const int64_t n = io.num_swarms * P, k = b * P + i;
         io.rng[0 * n + k] = rng.d;
@@ -126,23 +128,23 @@ __global__ void __launch_bounds__(kStreamChunk) k_stream_init(const ChainConsts<
         io.rng[4 * n + k] = rng.v3;
         io.rng[5 * n + k] = rng.v4;
     }
-    stream_publish_chunk<J>(io, b, c, sh, active ? ordered_key(pbf) : 0xFFFFFFFFu, pl);
+    stream_publish_chunk<Topo>(io, b, c, sh, active ? ordered_key(pbf) : 0xFFFFFFFFu, pl);
     if (c == 0 && threadIdx.x == 0) io.gkey[(int64_t)(io.t & 1) * io.num_swarms + b] = 0xFFFFFFFFu;
 }
 
 template <class Topo, int MODE, int TERMS>
 __global__ void __launch_bounds__(kStreamChunk) k_stream_step(const ChainConsts<Topo::J> cc, const StreamIO io)
 {
-    constexpr int J = Topo::J;
-    constexpr int D = 3 * J;
+    constexpr int J = Topo::J, A = Topo::A;
+    constexpr int D = Topo::D;
     const int64_t b = blockIdx.x / io.C;
     const int c = blockIdx.x % io.C;
     const int i = c * kStreamChunk + threadIdx.x;
     const bool active = i < io.P;
     const int64_t P = io.P;
-    __shared__ SwarmShared<J> sh;
-    stage_swarm_inputs<J>(cc, io.targets, io.start_pose, b, sh);
-    stream_resolve_gbest<J>(io, b, c, sh);
+    __shared__ SwarmShared<Topo> sh;
+    stage_swarm_inputs<Topo>(cc, io.targets, io.start_pose, b, sh);
+    stream_resolve_gbest<Topo>(io, b, c, sh);
     __syncthreads();
 
     const Planes pl(io.state + b * 3 * D * P, D, (int)P, i);
@@ -165,44 +167,45 @@ __global__ void __launch_bounds__(kStreamChunk) k_stream_step(const ChainConsts<
         // update-all-then-evaluate with the same values and accumulation order,
         // while only a handful of angles are live at a time.
         const PsoCoef coef = pso_coef(cc);
-        FitnessAcc<Topo, MODE, TERMS> acc(cc);
+        FitnessFor<Topo, MODE, TERMS> acc(cc, sh.dh);
         // Loads are software-pipelined AHEAD nodes ahead (a ring of AHEAD+1
         // node slots in registers, indices resolved at compile time) and every
         // node ends in a scheduling barrier: left alone, the compiler hoists
         // all 9J loads to the top (256 VGPRs, one wave per SIMD,
         // latency-bound); one node ahead leaves HBM latency exposed.
         constexpr int AHEAD = (IKPSO_STREAM_AHEAD < J) ? IKPSO_STREAM_AHEAD : J;
-        float ring[AHEAD + 1][9];
+        float ring[AHEAD + 1][3 * A];
 #pragma unroll
         for (int s = 0; s < AHEAD; ++s)
 #pragma unroll
-            for (int ax = 0; ax < 3; ++ax) {
-                ring[s][ax] = pl.ld(0, 3 * s + ax);
-                ring[s][3 + ax] = pl.ld(1, 3 * s + ax);
-                ring[s][6 + ax] = pl.ld(2, 3 * s + ax);
+            for (int ax = 0; ax < A; ++ax) {
+                ring[s][ax] = pl.ld(0, A * s + ax);
+                ring[s][A + ax] = pl.ld(1, A * s + ax);
+                ring[s][2 * A + ax] = pl.ld(2, A * s + ax);
             }
 #pragma unroll
         for (int kn = 1; kn <= J; ++kn) {
-            float cx[3], cv[3], cpb[3];
+            float cx[A], cv[A], cpb[A];
             const int cs = (kn - 1) % (AHEAD + 1);
 #pragma unroll
-            for (int ax = 0; ax < 3; ++ax) {
+            for (int ax = 0; ax < A; ++ax) {
                 cx[ax] = ring[cs][ax];
-                cv[ax] = ring[cs][3 + ax];
-                cpb[ax] = ring[cs][6 + ax];
+                cv[ax] = ring[cs][A + ax];
+                cpb[ax] = ring[cs][2 * A + ax];
             }
             if (kn - 1 + AHEAD < J) {  // node kn + AHEAD (0-based kn - 1 + AHEAD)
                 const int nn = kn - 1 + AHEAD, ns = nn % (AHEAD + 1);
 #pragma unroll
-                for (int ax = 0; ax < 3; ++ax) {
-                    ring[ns][ax] = pl.ld(0, 3 * nn + ax);
-                    ring[ns][3 + ax] = pl.ld(1, 3 * nn + ax);
-                    ring[ns][6 + ax] = pl.ld(2, 3 * nn + ax);
+                for (int ax = 0; ax < A; ++ax) {
+                    ring[ns][ax] = pl.ld(0, A * nn + ax);
+                    ring[ns][A + ax] = pl.ld(1, A * nn + ax);
+                    ring[ns][2 * A + ax] = pl.ld(2, A * nn + ax);
                 }
             }
 #pragma unroll
-            for (int ax = 0; ax < 3; ++ax) {
-                const int d = 3 * (kn - 1) + ax;
+            for (int ax = 0; ax < A; ++ax) {
+                const int d = A * (kn - 1) + ax;
+                if (kMasked<Topo, TERMS> && !dim_free(cc, d)) continue;  // locked: stays at rest
                 pso_update<MODE>(cx[ax], cv[ax], cpb[ax], sh.g[d], coef, rng);
                 pl.st(1, d, cv[ax]);
                 if constexpr (TERMS & kTermUniformBounds)
@@ -211,7 +214,7 @@ __global__ void __launch_bounds__(kStreamChunk) k_stream_step(const ChainConsts<
                     cx[ax] = clamp_mode<MODE>(cx[ax], sh.lo[d], sh.hi[d]);
                 pl.st(0, d, cx[ax]);
             }
-            acc.node(cc, kn, cx[0], cx[1], cx[2], sh.rest + 3 * (kn - 1), sh.tgt + 3 * (kn - 1), nullptr);
+            acc.node(cc, kn, cx, sh.rest + A * (kn - 1), sh.tgt + 3 * (kn - 1), nullptr);
             __builtin_amdgcn_sched_barrier(0);
         }
         // updateLocalBests (src/kernel.cu:202-221)
@@ -247,31 +250,30 @@ __global__ void __launch_bounds__(kStreamChunk) k_stream_step(const ChainConsts<
         io.rng[4 * n + k] = rng.v3;
         io.rng[5 * n + k] = rng.v4;
     }
-    stream_publish_chunk<J>(io, b, c, sh, active ? ordered_key(pbf) : 0xFFFFFFFFu, pl);
+    stream_publish_chunk<Topo>(io, b, c, sh, active ? ordered_key(pbf) : 0xFFFFFFFFu, pl);
 }
 
-template <class Topo, int MODE>
+template <class Topo, int MODE, int TERMS>
 __global__ void __launch_bounds__(kStreamChunk) k_stream_finalize(const ChainConsts<Topo::J> cc, const StreamIO io)
 {
-    constexpr int J = Topo::J;
-    constexpr int D = 3 * J;
+    constexpr int D = Topo::D;
     const int64_t b = blockIdx.x / io.C;
     const int c = blockIdx.x % io.C;
     const int i = c * kStreamChunk + threadIdx.x;
     const int64_t P = io.P;
-    __shared__ SwarmShared<J> sh;
-    stage_swarm_inputs<J>(cc, io.targets, io.start_pose, b, sh);
-    const uint32_t gkey = stream_resolve_gbest<J>(io, b, c, sh);
+    __shared__ SwarmShared<Topo> sh;
+    stage_swarm_inputs<Topo>(cc, io.targets, io.start_pose, b, sh);
+    const uint32_t gkey = stream_resolve_gbest<Topo>(io, b, c, sh);
     __syncthreads();
     if (c == 0) {
         // Coordinates result (updateGlobalBestCoordsKernel) + fitness + residual
-        for (int d = threadIdx.x; d < D; d += blockDim.x) io.out_angles[b * D + d] = sh.g[d];
+        for (int d = threadIdx.x; d < D; d += blockDim.x) store_angles<Topo>(cc, io.out_angles, b, d, sh.g[d]);
         if (threadIdx.x == 0 && io.out_fitness) io.out_fitness[b] = key_to_float(gkey);
         if (io.out_residual && threadIdx.x < 64) {
             float g[D];
 #pragma unroll
             for (int d = 0; d < D; ++d) g[d] = sh.g[d];
-            const float r = residual<Topo, MODE>(cc, g, sh.tgt);
+            const float r = residual<Topo, MODE, TERMS>(cc, g, sh.tgt, sh.dh);
             if (threadIdx.x == 0) io.out_residual[b] = r;
         }
     }
@@ -300,7 +302,7 @@ inline hipError_t run_stream(const ChainHost& ch, StreamIO io, int iterations, h
         hipLaunchKernelGGL((k_stream_step<Topo, MODE, TERMS>), grid, threads, 0, stream, cc, io);
     }
     io.t = iterations + 1;
-    hipLaunchKernelGGL((k_stream_finalize<Topo, MODE>), grid, threads, 0, stream, cc, io);
+    hipLaunchKernelGGL((k_stream_finalize<Topo, MODE, TERMS>), grid, threads, 0, stream, cc, io);
     return hipGetLastError();
 }
 
@@ -308,16 +310,19 @@ template <class Topo, int MODE>
 inline hipError_t run_stream_terms(const ChainHost& ch, const StreamIO& io, int iterations, hipStream_t stream)
 {
     // Same term specialisation as run_resident.
-    const int terms = (ch.use_posref ? kTermPosRef : 0) | (ch.use_penalty ? kTermPenalty : 0) |
-                      (ch.uniform_bounds ? kTermUniformBounds : 0) | (ch.num_coll > 0 ? kTermColliders : 0);
-    if constexpr (!Topo::kGeneric && MODE == IKPSO_ARITH_FAST) {
+    const int terms = term_set(ch);
+    hipError_t err = hipSuccess;
+    if (dh_terms<Topo>(terms, &err,
+                       [&](auto t) { return run_stream<Topo, MODE, decltype(t)::value>(ch, io, iterations, stream); }))
+        return err;
+    if constexpr (!Topo::kGeneric && !Topo::kDH && MODE == IKPSO_ARITH_FAST) {
         if (terms == kTermUniformBounds) return run_stream<Topo, MODE, kTermUniformBounds>(ch, io, iterations, stream);
         if (terms == (kTermUniformBounds | kTermPenalty))
             return run_stream<Topo, MODE, kTermUniformBounds | kTermPenalty>(ch, io, iterations, stream);
     }
     (void)terms;
-    if (ch.num_coll > 0) return run_stream<Topo, MODE, kTermRuntime | kTermColliders>(ch, io, iterations, stream);
-    return run_stream<Topo, MODE, kTermRuntime>(ch, io, iterations, stream);
+    return with_runtime_terms<Topo>(
+        ch, [&](auto t) { return run_stream<Topo, MODE, decltype(t)::value>(ch, io, iterations, stream); });
 }
 
 }  // namespace ikpso

@@ -39,29 +39,44 @@ __device__ __forceinline__ void store_rng(const Rng& r, ikpso_rng_state* p)
 // iteration stops the compiler from hoisting them into registers): ~100
 // loop-invariant uniforms held in SGPRs/VGPRs across the loop spill, while a
 // broadcast ds_read costs one LDS cycle.
-template <int J>
+template <class Topo>
 struct SwarmShared {
-    float lo[3 * J], hi[3 * J];  // clamp bounds
-    float rest[3 * J];           // warm start + angle-term reference
+    static constexpr int D = Topo::D, J = Topo::J;
+    float lo[D], hi[D];          // clamp bounds
+    float rest[D];               // warm start + angle-term reference
     float tgt[3 * J];            // effector targets per node (k-1), 0 elsewhere
-    float g[3 * J];              // global-best vector
+    float g[D];                  // global-best vector
+    float dh[Topo::kDH ? 12 * J + 4 : 1];  // folded-chain constants (TopoDH)
     uint32_t key[2][16];         // per-wave argmin, double-buffered by parity
     int32_t idx[2][16];
 };
 
-template <int J>
-__device__ __forceinline__ void stage_swarm_inputs(const ChainConsts<J>& cc, const float* targets,
-                                                   const float* start_pose, int64_t b, SwarmShared<J>& sh)
+// start_pose: [B][dfree] over the free dimensions (the chain's mask).
+template <class Topo>
+__device__ __forceinline__ void stage_swarm_inputs(const ChainConsts<Topo::J>& cc, const float* targets,
+                                                   const float* start_pose, int64_t b, SwarmShared<Topo>& sh)
 {
-    constexpr int D = 3 * J;
+    constexpr int D = Topo::D, J = Topo::J;
     const float* t = targets ? targets + b * (int64_t)cc.num_eff * 3 : nullptr;
     for (int d = threadIdx.x; d < D; d += blockDim.x) {
         sh.lo[d] = cc.lo[d];
         sh.hi[d] = cc.hi[d];
-        sh.rest[d] = start_pose ? start_pose[b * D + d] : cc.rest[d];
-        const int s = cc.eff_slot[d / 3 + 1];
-        sh.tgt[d] = t ? (s >= 0 ? t[3 * s + d % 3] : 0.0f) : cc.tgt0[d];
+        sh.rest[d] = start_pose && dim_free(cc, d) ? start_pose[b * cc.dfree + dim_rank(cc, d)] : cc.rest[d];
     }
+    for (int n = threadIdx.x; n < 3 * J; n += blockDim.x) {
+        const int s = cc.eff_slot[n / 3 + 1];
+        sh.tgt[n] = t ? (s >= 0 ? t[3 * s + n % 3] : 0.0f) : cc.tgt0[n];
+    }
+    if constexpr (Topo::kDH)
+        for (int n = threadIdx.x; n < 12 * J + 4; n += blockDim.x) sh.dh[n] = cc.aux[cc.dh_off + n];
+}
+
+// The swarm's answer over the free dimensions: out[b][dfree] from the kernel's
+// D-vector g (every thread of the calling workgroup; lanes < D write).
+template <class Topo>
+__device__ __forceinline__ void store_angles(const ChainConsts<Topo::J>& cc, float* out, int64_t b, int d, float g)
+{
+    if (d < Topo::D && dim_free(cc, d)) out[b * cc.dfree + dim_rank(cc, d)] = g;
 }
 
 __device__ __forceinline__ void compiler_fence() { asm volatile("" ::: "memory"); }
@@ -114,8 +129,8 @@ __device__ __forceinline__ int lane_id_here()
     return lane;
 }
 
-template <int J>
-__device__ __forceinline__ uint32_t swarm_argmin(SwarmShared<J>& sh, int par, uint32_t key, int* out_idx)
+template <class SH>
+__device__ __forceinline__ uint32_t swarm_argmin(SH& sh, int par, uint32_t key, int* out_idx)
 {
     const int lane = lane_id_here(), wave = wave_id();
     const int nwaves = blockDim.x >> 6;
@@ -134,14 +149,59 @@ __device__ __forceinline__ uint32_t swarm_argmin(SwarmShared<J>& sh, int par, ui
 
 // sh.g = local best of particle `idx` (updateGlobalBestCoordsKernel,
 // src/kernel.cu:268-277), copied by the first wave; the caller barriers.
-template <int J, int BLOCK>
-__device__ __forceinline__ void copy_gbest(SwarmShared<J>& sh, const float* s_pb, int idx)
+template <class Topo, int BLOCK>
+__device__ __forceinline__ void copy_gbest(SwarmShared<Topo>& sh, const float* s_pb, int idx)
 {
-    constexpr int D = 3 * J;
+    constexpr int D = Topo::D;
     static_assert(D <= 64, "one wave copies the global best");
     if (wave_id() == 0) {
         const int lane = lane_id_here();
         if (lane < D) sh.g[lane] = s_pb[lane * BLOCK + idx];
+    }
+}
+
+// Term set of a chain for the kernel specialisation (see FitnessAcc): a masked
+// chain carries kTermMask, which only the masked runtime-term builds match.
+inline int term_set(const ChainHost& ch)
+{
+    return (ch.use_posref ? kTermPosRef : 0) | (ch.use_penalty ? kTermPenalty : 0) |
+           (ch.uniform_bounds ? kTermUniformBounds : 0) | (ch.num_coll > 0 ? kTermColliders : 0) |
+           (ch.masked ? kTermMask : 0);
+}
+
+// The folded chain's builds: FAST, bounds uniform or not, penalty or not (it has
+// no distance, collider or mask term).  Returns false for another term set.
+template <class Topo, class F>
+inline bool dh_terms(int terms, hipError_t* err, F&& f)
+{
+    if constexpr (Topo::kDH) {
+        switch (terms) {
+        case kTermUniformBounds: *err = f(std::integral_constant<int, kTermUniformBounds>{}); return true;
+        case kTermUniformBounds | kTermPenalty:
+            *err = f(std::integral_constant<int, kTermUniformBounds | kTermPenalty>{});
+            return true;
+        case 0: *err = f(std::integral_constant<int, 0>{}); return true;
+        case kTermPenalty: *err = f(std::integral_constant<int, kTermPenalty>{}); return true;
+        default: break;
+        }
+    }
+    (void)terms;
+    (void)err;
+    return false;
+}
+
+// Visit the runtime-term build for a chain: kTermRuntime plus the collider
+// block and the axis mask when the chain has them (the folded chain has neither).
+template <class Topo, class F>
+inline hipError_t with_runtime_terms(const ChainHost& ch, F&& f)
+{
+    if constexpr (Topo::kDH) {  // every term set of a folded chain has its own build (dh_terms)
+        return hipErrorNotSupported;
+    } else {
+        if (ch.num_coll > 0 && ch.masked) return f(std::integral_constant<int, kTermRuntime | kTermColliders | kTermMask>{});
+        if (ch.num_coll > 0) return f(std::integral_constant<int, kTermRuntime | kTermColliders>{});
+        if (ch.masked) return f(std::integral_constant<int, kTermRuntime | kTermMask>{});
+        return f(std::integral_constant<int, kTermRuntime>{});
     }
 }
 
@@ -174,6 +234,18 @@ inline bool visit_topology(const ChainHost& ch, F&& f)
         break;
     case TopoKind::Generic:
         break;
+    case TopoKind::DH:
+        switch (ch.J) {  // free angles of a folded serial chain (DH arms: 3-12)
+#if IKPSO_WITH_OTHERS
+#define IKPSO_D(n) \
+    case n: f(TopoDH<n>{}); return true;
+            IKPSO_D(3) IKPSO_D(4) IKPSO_D(5) IKPSO_D(6) IKPSO_D(7) IKPSO_D(8) IKPSO_D(9) IKPSO_D(10) IKPSO_D(11)
+                IKPSO_D(12)
+#undef IKPSO_D
+#endif
+        default: break;
+        }
+        return false;  // no generic fallback: the caller keeps the Euler chain
     }
 #if IKPSO_WITH_OTHERS
     switch (ch.J) {  // any tree: runtime parent indices

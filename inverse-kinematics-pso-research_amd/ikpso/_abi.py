@@ -72,9 +72,10 @@ COLLIDER_DTYPE = np.dtype(
 )
 assert COLLIDER_DTYPE.itemsize == 48
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 FLAG_POSREF_NODE_SLOT = 1  # IKPSO_FLAG_POSREF_NODE_SLOT
+FLAG_NO_FOLD = 2  # IKPSO_FLAG_NO_FOLD
 
 
 # ------------------------------------------------------------ ctypes structs
@@ -116,6 +117,7 @@ class SolverDesc(ctypes.Structure):
         ("colliders", ctypes.c_void_p),
         ("collider_count", ctypes.c_int32),
         ("flags", ctypes.c_int32),
+        ("axis_mask", ctypes.c_void_p),  # ABI >= 4
     ]
 
 

@@ -24,6 +24,12 @@ inverse is folded into the next K.  The last node is the tool effector.
 The chain then runs through the same solver kernels as any reference scene;
 serial chains of 6, 7 and 20 nodes with a tip effector have specialised
 kernels.  Joint angles map back as theta_i = z_node - r_i.
+
+With the joint-axis mask (`DHArm.axis_mask`, ABI >= 4) only the joint nodes' z
+angles are PSO dimensions: D = number of joints, locked angles take no draws
+and no update, and a FAST solver folds the arm into one sincos per joint
+(TopoDH, include/ikpso.h).  Without it every locked angle is emulated by equal
+clamp bounds and still costs draws, an update and a sincos (3 per node).
 """
 from __future__ import annotations
 
@@ -33,6 +39,13 @@ from typing import List, Optional, Sequence
 import numpy as np
 
 from .scene import EffectorNode, Node, OriginNode, TargetNode
+
+
+# KUKA LBR iiwa 14 R820 (standard DH; lengths in m, joint limits in rad): the
+# 7-joint arm the DH tests and bench.py --config dh7 use.
+IIWA14 = dict(a=[0.0] * 7, alpha=[-np.pi / 2, np.pi / 2, np.pi / 2, -np.pi / 2, -np.pi / 2, np.pi / 2, 0.0],
+              d=[0.36, 0.0, 0.42, 0.0, 0.4, 0.0, 0.126],
+              limits=np.radians([170.0, 120.0, 170.0, 120.0, 170.0, 120.0, 175.0]))
 
 
 def _rx(a):
@@ -97,15 +110,35 @@ class DHArm:
         """Scalar angles of the node table (3 per node, most locked)."""
         return 3 * self.origin.count_children()
 
+    @property
+    def joints(self) -> int:
+        """DH joints = the free dimensions under `axis_mask`."""
+        return len(self.joint_nodes)
+
+    @property
+    def axis_mask(self) -> np.ndarray:
+        """Joint-axis mask of the node table ([node_count] uint8, bit c = Euler
+        angle c free): each joint node's z angle, nothing else."""
+        ids = {id(n) for n in self.joint_nodes}
+        nodes = list(self.origin.dfs())
+        return np.array([0] + [4 if id(n) in ids else 0 for n in nodes[1:]], dtype=np.uint8)
+
     def joint_angles(self, coords: np.ndarray) -> np.ndarray:
-        """theta per DH joint from a solver angle vector (ToCoords order)."""
-        coords = np.asarray(coords, dtype=np.float64).reshape(-1, 3)
+        """theta per DH joint from a solver angle vector: ToCoords order (3 per
+        node), or the masked solver's D = joints free angles."""
+        coords = np.asarray(coords, dtype=np.float64).reshape(-1)
+        if coords.size == self.joints:
+            return coords - self.z_offset
+        coords = coords.reshape(-1, 3)
         nodes = list(self.origin.dfs())[1:]
         idx = {id(n): i for i, n in enumerate(nodes)}
         return np.array([coords[idx[id(n)], 2] for n in self.joint_nodes]) - self.z_offset
 
-    def coords(self, theta: Sequence[float]) -> np.ndarray:
-        """Solver angle vector (ToCoords order) for joint angles theta."""
+    def coords(self, theta: Sequence[float], masked: bool = False) -> np.ndarray:
+        """Solver angle vector for joint angles theta: ToCoords order, or with
+        `masked` the D = joints free angles of the axis-masked solver."""
+        if masked:
+            return (np.asarray(theta, dtype=np.float64) + self.z_offset).astype(np.float32)
         nodes = list(self.origin.dfs())[1:]
         out = np.concatenate([n.rotation for n in nodes]).astype(np.float64).reshape(-1, 3)
         idx = {id(n): i for i, n in enumerate(nodes)}
@@ -158,3 +191,9 @@ def dh_arm(a: Sequence[float], alpha: Sequence[float], d: Sequence[float], theta
         else:
             k = _rx(float(alpha[i]))
     return DHArm(origin, joints, np.asarray(offsets, dtype=np.float64), tool, tgt)
+
+
+def iiwa14(target=(0.0, 0.0, 0.0)) -> DHArm:
+    """The IIWA14 arm as a node tree (joint limits +-limits)."""
+    lim = IIWA14["limits"]
+    return dh_arm(IIWA14["a"], IIWA14["alpha"], IIWA14["d"], -lim, lim, target=target)

@@ -171,7 +171,7 @@ class BatchSolver:
     def __init__(self, chain: np.ndarray, particles: int, pso: PSOConfig = MAIN_PSO,
                  fit: FitnessConfig = MAIN_FITNESS, arith: str = "fast", positions=None,
                  limit_weight: float = 0.0, soft_lo=None, soft_hi=None, kernel: str = "auto", colliders=None,
-                 posref_node_slot: bool = False):
+                 posref_node_slot: bool = False, axis_mask=None, fold: bool = True):
         self._lib = _abi.load()
         if chain.dtype != NODE_DTYPE:
             raise TypeError("chain must be an ikpso NODE_DTYPE array")
@@ -193,7 +193,13 @@ class BatchSolver:
         desc.limit_weight = float(limit_weight)
         desc.soft_lo = _any_ptr(None if soft_lo is None else np.asarray(soft_lo, np.float32), keep)
         desc.soft_hi = _any_ptr(None if soft_hi is None else np.asarray(soft_hi, np.float32), keep)
-        desc.flags = _abi.FLAG_POSREF_NODE_SLOT if posref_node_slot else 0
+        desc.flags = (_abi.FLAG_POSREF_NODE_SLOT if posref_node_slot else 0) | (0 if fold else _abi.FLAG_NO_FOLD)
+        if axis_mask is not None:  # [node_count] uint8: bit c = Euler angle c of node k is free
+            m = np.ascontiguousarray(axis_mask, dtype=np.uint8)
+            if m.shape != (self.chain.shape[0],):
+                raise ValueError(f"axis_mask must have one entry per node ({self.chain.shape[0]})")
+            desc.axis_mask = _any_ptr(m, keep)
+        self.axis_mask = None if axis_mask is None else np.array(axis_mask, dtype=np.uint8)
         if colliders is not None and len(colliders):
             boxes = _colliders(colliders)
             desc.colliders = _any_ptr(boxes, keep)
@@ -286,7 +292,7 @@ class BatchSolver:
         for t, name in ((angles, "angles"), (targets, "targets"), (rest, "rest")):
             self._check_tensor(t, name, angles.device)
         fit = torch.empty((n,), dtype=torch.float32, device=angles.device)
-        pos = torch.empty((n, self.dof // 3, 3), dtype=torch.float32, device=angles.device)
+        pos = torch.empty((n, self.chain.shape[0] - 1, 3), dtype=torch.float32, device=angles.device)
         _abi.check(self._lib.ikpso_solver_evaluate(self._h, _dev_ptr(angles), _dev_ptr(targets), _dev_ptr(rest), n,
                                                    _dev_ptr(fit), _dev_ptr(pos), _stream_handle(stream)),
                    "ikpso_solver_evaluate")

@@ -8,6 +8,13 @@
        soft joint-limit penalty lambda=10 (limits +-pi/2, clamp +-pi), P=4096,
        I=500, B=8192
 
+and the DH rows of SURVEY.md §8(f) row 4 (not BASELINE configs; bench.py
+--config dh7*): the 7-joint KUKA iiwa 14 as a DH arm, 4096 reachable targets
+(tool positions of seeded joint angles), P=1024, I=500, position-only fitness:
+    dh7         joint-axis mask, D = 7 (FAST: the folded chain)
+    dh7-nofold  joint-axis mask, D = 7, Euler kernels skipping locked angles
+    dh7-locked  no mask: locked angles emulated by equal clamp bounds, D = 33
+
 Particle seeds are global: swarm b, particle i uses curand_init(b*P + i), so
 swarm 0 of config 3 is the reference's own solve and any sharding of the batch
 reproduces the same per-swarm results.
@@ -77,20 +84,38 @@ class Workload:
     soft_hi: Optional[np.ndarray] = None
     description: str = ""
     extra: dict = field(default_factory=dict)
+    axis_mask: Optional[np.ndarray] = None
+    fold: bool = True
 
     @property
     def dof(self) -> int:
+        if self.axis_mask is not None:
+            return int(sum(bin(int(m) & 7).count("1") for m in self.axis_mask[1:]))
         return 3 * (self.chain.shape[0] - 1)
 
     def targets(self, first_swarm: int, count: int) -> np.ndarray:
         if self.name == "config5":
             return shell_targets(first_swarm, count)
+        if self.name.startswith("dh7"):
+            return dh7_targets(first_swarm, count)
         if self.name in ("config1", "config2"):
             return np.repeat(RESET_TARGETS[None], count, axis=0)
         return batch_targets(first_swarm, count)
 
 
-def workload(n: int) -> Workload:
+def dh7_targets(first_swarm: int, count: int) -> np.ndarray:
+    """Reachable iiwa tool positions: the DH product of joint angles U(-0.8, 0.8)
+    x limits from splitmix64(0x5EED7000 + b): [count, 1, 3] float32."""
+    from .dh import IIWA14, dh_forward
+
+    b = np.arange(first_swarm, first_swarm + count, dtype=np.uint64)
+    u = unit_floats(splitmix64_stream(np.uint64(0x5EED7000) + b, 7))
+    th = (2.0 * u - 1.0) * 0.8 * IIWA14["limits"][None]
+    p = np.array([dh_forward(t, IIWA14["d"], IIWA14["a"], IIWA14["alpha"]) for t in th])
+    return p.astype(np.float32)[:, None, :]
+
+
+def workload(n) -> Workload:
     pso = PSOConfig(0.5, 0.5, 1.25, 500)  # src/Main.cpp:130 coefficients
     if n in (1, 2, 3, 4):
         chain = reference_scene(reset=True).origin.to_cuda()
@@ -112,4 +137,18 @@ def workload(n: int) -> Workload:
                         soft_hi=soft,
                         description="20-joint serial chain (D=60), tip effector, 4096 particles, 500 iterations, "
                                     "soft joint-limit penalty")
+    if isinstance(n, str) and n in ("dh7", "dh7-nofold", "dh7-locked"):
+        from .dh import iiwa14
+
+        arm = iiwa14()
+        mask = None if n == "dh7-locked" else arm.axis_mask
+        how = {"dh7": "joint-axis mask (D=7), folded chain",
+               "dh7-nofold": "joint-axis mask (D=7), Euler kernels",
+               "dh7-locked": "locked axes by equal clamp bounds (D=33)"}[n]
+        return Workload(n, arm.origin.to_cuda(), 1024, 500, 4096, pso, FitnessConfig(0.0, 0.0, 0.1),
+                        description=f"7-joint KUKA iiwa 14 DH arm as 11 nodes, {how}, 4096 reachable targets, "
+                                    "1024 particles, 500 iterations, position-only fitness",
+                        axis_mask=mask, fold=n == "dh7")
+    if isinstance(n, str) and n.isdigit():
+        return workload(int(n))
     raise ValueError(f"no BASELINE config {n}")

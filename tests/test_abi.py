@@ -44,7 +44,7 @@ def test_compat_symbols_exported():
 
 def test_abi_version_and_strings():
     lib = _abi.load()
-    assert lib.ikpso_abi_version() == 3
+    assert lib.ikpso_abi_version() == 4
     assert lib.ikpso_status_string(0) == b"ok"
     assert lib.ikpso_status_string(2) == b"unsupported configuration"
 
@@ -60,9 +60,9 @@ def test_struct_layouts_match_header():
       printf("%zu %zu %zu %zu %zu %zu %zu\n", offsetof(ikpso_node, position), offsetof(ikpso_node, rotation),
              offsetof(ikpso_node, max_rotation), offsetof(ikpso_node, min_rotation), offsetof(ikpso_node, length),
              offsetof(ikpso_node, target_position), offsetof(ikpso_collider, quat));
-      printf("%zu %zu %zu %zu %zu\n", sizeof(ikpso_solver_desc), offsetof(ikpso_solver_desc, positions),
+      printf("%zu %zu %zu %zu %zu %zu\n", sizeof(ikpso_solver_desc), offsetof(ikpso_solver_desc, positions),
              offsetof(ikpso_solver_desc, soft_hi), offsetof(ikpso_solver_desc, colliders),
-             offsetof(ikpso_solver_desc, collider_count));
+             offsetof(ikpso_solver_desc, collider_count), offsetof(ikpso_solver_desc, axis_mask));
       return 0; }
     '''
     with tempfile.TemporaryDirectory() as td:
@@ -82,6 +82,7 @@ def test_struct_layouts_match_header():
     assert d[0] == ctypes.sizeof(_abi.SolverDesc)
     assert d[1] == _abi.SolverDesc.positions.offset and d[2] == _abi.SolverDesc.soft_hi.offset
     assert d[3] == _abi.SolverDesc.colliders.offset and d[4] == _abi.SolverDesc.collider_count.offset
+    assert d[5] == _abi.SolverDesc.axis_mask.offset
     assert _abi.COLLIDER_DTYPE.fields["quat"][1] == offs[6]
 
 

@@ -52,30 +52,37 @@ __device__ inline int ulps(float a, float b)
     return ia > ib ? ia - ib : ib - ia;
 }
 
-struct Stats { unsigned long long bad[4]; unsigned maxulp[4]; float maxabs[4]; };
+#define NV 6
+struct Stats { unsigned long long bad[NV]; unsigned maxulp[NV]; float maxabs[NV]; };
 
 __global__ void probe(float lo, float hi, unsigned long long n, unsigned seed, Stats* st, unsigned* bop_bad)
 {
-    __shared__ unsigned long long sbad[4];
-    __shared__ unsigned smax[4];
-    __shared__ float sabs[4];
-    if (threadIdx.x < 4) { sbad[threadIdx.x] = 0; smax[threadIdx.x] = 0; sabs[threadIdx.x] = 0; }
+    __shared__ unsigned long long sbad[NV];
+    __shared__ unsigned smax[NV];
+    __shared__ float sabs[NV];
+    if (threadIdx.x < NV) { sbad[threadIdx.x] = 0; smax[threadIdx.x] = 0; sabs[threadIdx.x] = 0; }
     __syncthreads();
-    unsigned long long bad[4] = {0, 0, 0, 0};
-    unsigned mu[4] = {0, 0, 0, 0};
-    float ma[4] = {0, 0, 0, 0};
+    unsigned long long bad[NV] = {};
+    unsigned mu[NV] = {};
+    float ma[NV] = {};
     for (unsigned long long i = blockIdx.x * (unsigned long long)blockDim.x + threadIdx.x; i < n;
          i += (unsigned long long)gridDim.x * blockDim.x) {
         unsigned h = (unsigned)i * 2654435761u ^ seed;
         h ^= h >> 13; h *= 0x5bd1e995u; h ^= h >> 15;
         const float x = lo + (hi - lo) * ((h >> 8) * (1.0f / 16777216.0f));
         const float ts = (float)sin((double)x), tc = (float)cos((double)x);
-        float s[4], c[4];
+        float s[NV], c[NV];
         ikpso::sincos_fast(x, &s[0], &c[0]);
         s[1] = __sinf(x); c[1] = __cosf(x);
         sincos_v2(x, &s[2], &c[2]);
         sincos_v3(x, &s[3], &c[3]);
-        for (int v = 0; v < 4; ++v) {
+        {   // hardware v_sin/v_cos on x / 2pi (revolutions), no range reduction
+            const float t = x * 0.159154943091895336f;
+            s[4] = __builtin_amdgcn_sinf(t); c[4] = __builtin_amdgcn_cosf(t);
+            const float tf = __builtin_amdgcn_fractf(t);  // with v_fract_f32 first
+            s[5] = __builtin_amdgcn_sinf(tf); c[5] = __builtin_amdgcn_cosf(tf);
+        }
+        for (int v = 0; v < NV; ++v) {
             if (s[v] != ts || c[v] != tc) bad[v]++;
             const float ea = fmaxf(fabsf(s[v] - ts), fabsf(c[v] - tc));
             ma[v] = fmaxf(ma[v], ea);
@@ -89,13 +96,13 @@ __global__ void probe(float lo, float hi, unsigned long long n, unsigned seed, S
         if (__builtin_amdgcn_bitop3_b32(a, b, cc, 0x96) != (a ^ b ^ cc)) atomicAdd(bop_bad, 1u);
         if (__builtin_amdgcn_bitop3_b32(a, b, cc, 0x78) != (a ^ (b & cc))) atomicAdd(bop_bad + 1, 1u);
     }
-    for (int v = 0; v < 4; ++v) {
+    for (int v = 0; v < NV; ++v) {
         atomicAdd(&sbad[v], bad[v]);
         atomicMax(&smax[v], mu[v]);
         atomicMax((int*)&sabs[v], __float_as_int(ma[v]));
     }
     __syncthreads();
-    if (threadIdx.x < 4) {
+    if (threadIdx.x < NV) {
         atomicAdd(&st->bad[threadIdx.x], sbad[threadIdx.x]);
         atomicMax(&st->maxulp[threadIdx.x], smax[threadIdx.x]);
         atomicMax((int*)&st->maxabs[threadIdx.x], __float_as_int(sabs[threadIdx.x]));
@@ -104,9 +111,9 @@ __global__ void probe(float lo, float hi, unsigned long long n, unsigned seed, S
 
 int main()
 {
-    const char* names[4] = {"sincos_fast (current FAST)", "__sinf/__cosf (v_sin/v_cos)", "sincos_v2 (bitop3 signs)",
-                            "sincos_v3 (2-fma reduction)"};
-    const float ranges[3][2] = {{-7.0f, 7.0f}, {0.0f, 6.2831855f}, {-100.0f, 100.0f}};
+    const char* names[NV] = {"sincos_fast (current FAST)", "__sinf/__cosf", "sincos_v2 (bitop3 signs)",
+                             "sincos_v3 (2-fma reduction)", "v_sin/v_cos(x/2pi)", "v_sin/v_cos(fract(x/2pi))"};
+    const float ranges[4][2] = {{-7.0f, 7.0f}, {0.0f, 6.2831855f}, {-3.1415927f, 3.1415927f}, {-100.0f, 100.0f}};
     Stats* st; unsigned* bb;
     hipMalloc(&st, sizeof(Stats)); hipMalloc(&bb, 8);
     for (auto& r : ranges) {
@@ -116,7 +123,7 @@ int main()
         Stats h; unsigned hb[2];
         hipMemcpy(&h, st, sizeof h, hipMemcpyDeviceToHost); hipMemcpy(hb, bb, 8, hipMemcpyDeviceToHost);
         printf("x in [%g, %g], %llu samples; bitop3 mismatches xor3=%u a^(b&c)=%u\n", r[0], r[1], n, hb[0], hb[1]);
-        for (int v = 0; v < 4; ++v)
+        for (int v = 0; v < NV; ++v)
             printf("  %-32s not-correctly-rounded %6.3f%%  max ulp %u  max abs %.3g\n", names[v],
                    100.0 * h.bad[v] / n, h.maxulp[v], h.maxabs[v]);
     }

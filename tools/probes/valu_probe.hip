@@ -59,6 +59,12 @@ __global__ void __launch_bounds__(1024) k_op(float* out, int iters, float sa, fl
                 if constexpr (OP == 30) asm volatile("v_add_u32 %0, %0, %1" : "+v"(u[c]) : "v"(ua));
                 if constexpr (OP == 31) asm volatile("v_xad_u32 %0, %0, %1, %2" : "+v"(u[c]) : "v"(ua), "v"(ub));
                 if constexpr (OP == 32) asm volatile("v_cvt_f32_u32_e64 %0, %1" : "=v"(f[c]) : "v"(u[c]));
+                if constexpr (OP == 33) f[c] = __builtin_amdgcn_sinf(f[c]);       // v_sin_f32 (transcendental)
+                if constexpr (OP == 34) {                                          // half v_sin, half v_fma:
+                    if (c & 1) f[c] = __builtin_fmaf(f[c], va, vb);                // does TRANS overlap VALU?
+                    else f[c] = __builtin_amdgcn_sinf(f[c]);
+                }
+                if constexpr (OP == 35) f[c] = __builtin_amdgcn_cosf(f[c]);       // v_cos_f32
             }
     }
     float s = 0.f;
@@ -71,7 +77,7 @@ static const char* kNames[] = {
     "v_mul_f32 v,v", "v_mul_f32 v,s", "v_mul_f32 v,literal", "v_mul_f32 v,inline", "v_fmac_f32 v,v",
     "v_fma_f32 v,v,v", "v_fma_f32 v,s,s", "v_fmaak_f32 literal", "v_xor_b32 v,v", "v_lshlrev_b32 inline",
     "v_bitop3_b32 v,v,v", "v_add3_u32 v,v,v", "v_cvt_f32_u32 v", "v_med3_f32 v,v,v",
-    "v_lshrrev_b32 inline", "v_lshlrev_b32 inline 4", "v_lshlrev_b32 inline 1", "v_lshrrev_b32 inline 3", "v_add_u32 v,v (x+x)", "v_add_u32 literal", "v_alignbit_b32 v,0,28 (x<<4)", "v_lshl_add_u32 v,4,0", "v_lshl_or_b32 v,4,0", "v_bfe_i32 v,0,1", "v_and_b32 literal", "v_sub_f32 v,v", "v_max_f32 v,v", "v_mov_b32 v", "v_fmamk_f32 literal", "v_lshlrev_b32 v,v (vgpr amount)", "v_add_u32 v,v,v", "v_xad_u32 v,v,v", "v_cvt_f32_u32 e64"};
+    "v_lshrrev_b32 inline", "v_lshlrev_b32 inline 4", "v_lshlrev_b32 inline 1", "v_lshrrev_b32 inline 3", "v_add_u32 v,v (x+x)", "v_add_u32 literal", "v_alignbit_b32 v,0,28 (x<<4)", "v_lshl_add_u32 v,4,0", "v_lshl_or_b32 v,4,0", "v_bfe_i32 v,0,1", "v_and_b32 literal", "v_sub_f32 v,v", "v_max_f32 v,v", "v_mov_b32 v", "v_fmamk_f32 literal", "v_lshlrev_b32 v,v (vgpr amount)", "v_add_u32 v,v,v", "v_xad_u32 v,v,v", "v_cvt_f32_u32 e64", "v_sin_f32 v", "v_sin_f32 / v_fma_f32 1:1", "v_cos_f32 v"};
 
 
 template <int OP>
@@ -110,7 +116,7 @@ int main()
     const int blocks = cus * 8;
     void* out;
     hipMalloc(&out, (size_t)blocks * 1024 * 4);
-    run_all(blocks, out, std::make_integer_sequence<int, 33>{});
+    run_all(blocks, out, std::make_integer_sequence<int, 36>{});
     hipFree(out);
     return 0;
 }
