@@ -301,16 +301,27 @@ def main():
         vpu = None if streaming else valu_per_update(solver.kernel)
         valu = None
         if vpu:
-            ach = ups_launch * vpu["valu_lane_instr_per_update"] / kern_s / 1e12
-            valu = {"achieved": round(ach, 2), "peak": round(VALU_PEAK_TINSTR, 1), "unit": "Tlane-instr/s",
+            # issue slots: a transcendental (v_sin/v_cos) occupies the VALU for 4 of the 2-cycle issue slots
+            # of an ordinary op on gfx950 (tools/probes/valu_probe.hip: 8.1 vs 2.1 cycles per wave64 op)
+            trans = vpu.get("trans_lane_instr_per_update") or 0.0
+            slots = vpu["valu_lane_instr_per_update"] + 3.0 * trans
+            ach = ups_launch * slots / kern_s / 1e12
+            valu = {"achieved": round(ach, 2), "peak": round(VALU_PEAK_TINSTR, 1), "unit": "Tlane-slot/s",
                     "frac": round(ach / VALU_PEAK_TINSTR, 4),
-                    "instr_per_update": vpu["valu_lane_instr_per_update"], "source": vpu.get("source")}
+                    "instr_per_update": vpu["valu_lane_instr_per_update"], "trans_per_update": trans,
+                    "issue_slots_per_update": round(slots, 1), "source": vpu.get("source"),
+                    "note": "VALU issue roof: 78.6 T lane-slots/s = 256 CU x 4 SIMD x 32 lanes x 2.4 GHz (one "
+                            "wave64 op per 2 cycles per SIMD); SQ_INSTS_VALU lane-instructions per update with "
+                            "each transcendental counted as 4 slots"}
+        # the streaming kernels move x/v/pbest through HBM (HBM-bound); an on-chip kernel without a committed
+        # PMC profile is reported unmeasured rather than against the HBM formulation it does not use
+        on_chip_unmeasured = not streaming and not valu
         roofline = {
-            "bound": "valu" if valu else "hbm",
-            "achieved": valu["achieved"] if valu else round(alg_gbs, 1),
-            "peak": valu["peak"] if valu else HBM_PEAK_GBS,
-            "unit": valu["unit"] if valu else "GB/s",
-            "frac": valu["frac"] if valu else round(alg_gbs / HBM_PEAK_GBS, 4),
+            "bound": "valu" if valu or on_chip_unmeasured else "hbm",
+            "achieved": valu["achieved"] if valu else (None if on_chip_unmeasured else round(alg_gbs, 1)),
+            "peak": valu["peak"] if valu else (round(VALU_PEAK_TINSTR, 1) if on_chip_unmeasured else HBM_PEAK_GBS),
+            "unit": valu["unit"] if valu else ("Tlane-slot/s" if on_chip_unmeasured else "GB/s"),
+            "frac": valu["frac"] if valu else (None if on_chip_unmeasured else round(alg_gbs / HBM_PEAK_GBS, 4)),
             "traffic": round(vpu["hbm_bytes_per_update"] * ups_launch) if vpu else None,
             "kernel": solver.kernel + (" (I+2 launches per batch)" if streaming else " (one launch = one batch)"),
             "kernel_ms": round(kern_ms, 3),
@@ -375,6 +386,9 @@ def main():
         }
         if valu:
             line["roofline"]["valu"] = valu
+        elif on_chip_unmeasured:
+            line["roofline"]["note"] = (f"no committed rocprofv3 PMC profile of {solver.kernel} "
+                                        "(profiles/valu_per_update.json): VALU fraction unmeasured for this line")
         if cfg == 2:
             line["roofline"]["note"] = ("config 2 is one swarm on 4 of 256 CUs: latency-bound (SURVEY 8(d)), "
                                         "the chip-wide fraction is not a kernel-quality figure")

@@ -81,6 +81,16 @@ struct obj {
 typedef struct obj obj_t;
 #endif /* IKPSO_COMPAT_REFERENCE_TYPES */
 
+/* The caller's DEGREES_OF_FREEDOM, seen by the library (which is built for one
+ * value, -DDEGREES_OF_FREEDOM=N): calculatePSO reads `chain` and `result` with
+ * its own D, so a caller built with another D gets hipErrorInvalidValue
+ * instead of a silently wrong node count.  A weak definition in every caller
+ * translation unit that includes this header (the library's own build does
+ * not define it); a caller that never includes it is not checked. */
+#ifndef IKPSO_BUILDING_LIBRARY
+extern "C" __attribute__((weak, visibility("default"))) const int ikpso_compat_caller_dof = DEGREES_OF_FREEDOM;
+#endif
+
 hipError_t initGenerators(curandState_t* randoms, int size);
 hipError_t calculatePSO(float* particles, float* positions, float* bests, curandState_t* randoms, int size,
                         NodeCUDA* chain, PSOConfig psoConfig, FitnessConfig fitConfig, Coordinates* result,

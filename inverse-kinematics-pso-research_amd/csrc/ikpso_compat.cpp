@@ -1,8 +1,12 @@
 // ikpso_compat.cpp -- initGenerators / calculatePSO with the reference's
 // signatures (include/ikpso_compat.h), forwarding to the C ABI.
+#define IKPSO_BUILDING_LIBRARY
 #include "ikpso_compat.h"
 
 #include "ikpso.h"
+
+// Defined (weakly) by callers that include ikpso_compat.h: their DEGREES_OF_FREEDOM.
+extern "C" __attribute__((weak)) const int ikpso_compat_caller_dof;
 
 static_assert(sizeof(NodeCUDA) == sizeof(ikpso_node), "NodeCUDA layout");
 static_assert(sizeof(curandState_t) == sizeof(ikpso_rng_state), "curandState_t layout");
@@ -33,6 +37,10 @@ hipError_t calculatePSO(float* particles, float* positions, float* bests, curand
                         NodeCUDA* chain, PSOConfig psoConfig, FitnessConfig fitConfig, Coordinates* result,
                         obj_t* colliders, int colliderCount)
 {
+    // Coordinates and the node table are sized by the caller's DEGREES_OF_FREEDOM:
+    // refuse a caller compiled for another chain length
+    if (&ikpso_compat_caller_dof != nullptr && ikpso_compat_caller_dof != DEGREES_OF_FREEDOM)
+        return hipErrorInvalidConfiguration;
     const ikpso_pso_config pso{psoConfig._inertia, psoConfig._local, psoConfig._global, psoConfig._iterations};
     const ikpso_fitness_config fit{fitConfig.angleWeight, fitConfig.distanceWeight, fitConfig.errorThreshold};
     return to_hip(ikpso_calculate_pso(particles, positions, bests, reinterpret_cast<ikpso_rng_state*>(randoms), size,

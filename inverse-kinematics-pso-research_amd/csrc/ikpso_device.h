@@ -48,6 +48,9 @@
 #ifndef IKPSO_SINCOS_HW
 #define IKPSO_SINCOS_HW 1
 #endif
+#ifndef IKPSO_HW_TRIG_MAX_D
+#define IKPSO_HW_TRIG_MAX_D 30
+#endif
 
 
 namespace ikpso {
@@ -361,13 +364,26 @@ __device__ __forceinline__ Frame origin_frame(const float* m0)
 // FAST: closed-form local rotation Rx(a)Ry(b)Rz(c), then world = parent * local,
 // FMA contraction allowed.  For leaf nodes only the position is consumed and
 // the compiler drops the unused rotation entries.
-template <bool HW>
-__device__ __forceinline__ Frame child_frame_fast(const Frame& P, float a, float b, float c, float len)
+// Sines and cosines of a node's A angles, computed ahead of the node's FK
+// (FAST: swarm_step evaluates them one node early so the transcendental
+// latency hides under the previous node's FK).
+template <int A>
+struct NodeTrig {
+    float s[A], c[A];
+};
+
+template <bool HW, int A>
+__device__ __forceinline__ NodeTrig<A> node_trig(const float* ang)
 {
-    float sa, ca, sb, cb, sc, cc;
-    sincos_fast<HW>(a, &sa, &ca);
-    sincos_fast<HW>(b, &sb, &cb);
-    sincos_fast<HW>(c, &sc, &cc);
+    NodeTrig<A> t;
+#pragma unroll
+    for (int ax = 0; ax < A; ++ax) sincos_fast<HW>(ang[ax], &t.s[ax], &t.c[ax]);
+    return t;
+}
+
+__device__ __forceinline__ Frame child_frame_fast_sc(const Frame& P, float sa, float ca, float sb, float cb, float sc,
+                                                     float cc, float len)
+{
     const float p = sa * sb, q = ca * sb;
     const float l00 = cb * cc, l01 = -cb * sc, l02 = sb;
     const float l10 = p * cc + ca * sc, l11 = ca * cc - p * sc, l12 = -sa * cb;
@@ -388,18 +404,24 @@ __device__ __forceinline__ Frame child_frame_fast(const Frame& P, float a, float
     return W;
 }
 
-// FAST, interior nodes (the whole world rotation is consumed by the children):
-// apply Rx, Ry, Rz to the parent's columns in turn -- each is a plane rotation
-// of two columns (12 multiply-adds), 36 in all against 14 + 27 for building
-// the local matrix and multiplying it in.  Leaves, which only need the first
-// column, keep the closed form (the compiler then drops the other columns).
 template <bool HW>
-__device__ __forceinline__ Frame child_frame_fast_seq(const Frame& P, float a, float b, float c, float len)
+__device__ __forceinline__ Frame child_frame_fast(const Frame& P, float a, float b, float c, float len)
 {
     float sa, ca, sb, cb, sc, cc;
     sincos_fast<HW>(a, &sa, &ca);
     sincos_fast<HW>(b, &sb, &cb);
     sincos_fast<HW>(c, &sc, &cc);
+    return child_frame_fast_sc(P, sa, ca, sb, cb, sc, cc, len);
+}
+
+// FAST, interior nodes (the whole world rotation is consumed by the children):
+// apply Rx, Ry, Rz to the parent's columns in turn -- each is a plane rotation
+// of two columns (12 multiply-adds), 36 in all against 14 + 27 for building
+// the local matrix and multiplying it in.  Leaves, which only need the first
+// column, keep the closed form (the compiler then drops the other columns).
+__device__ __forceinline__ Frame child_frame_fast_seq_sc(const Frame& P, float sa, float ca, float sb, float cb,
+                                                         float sc, float cc, float len)
+{
     // * Rx(a): columns 1, 2 become (ca c1 + sa c2, ca c2 - sa c1)
     const float x01 = P.r01 * ca + P.r02 * sa, x02 = P.r02 * ca - P.r01 * sa;
     const float x11 = P.r11 * ca + P.r12 * sa, x12 = P.r12 * ca - P.r11 * sa;
@@ -423,6 +445,16 @@ __device__ __forceinline__ Frame child_frame_fast_seq(const Frame& P, float a, f
     W.py = P.py + len * W.r10;
     W.pz = P.pz + len * W.r20;
     return W;
+}
+
+template <bool HW>
+__device__ __forceinline__ Frame child_frame_fast_seq(const Frame& P, float a, float b, float c, float len)
+{
+    float sa, ca, sb, cb, sc, cc;
+    sincos_fast<HW>(a, &sa, &ca);
+    sincos_fast<HW>(b, &sb, &cb);
+    sincos_fast<HW>(c, &sc, &cc);
+    return child_frame_fast_seq_sc(P, sa, ca, sb, cb, sc, cc, len);
 }
 
 // REFERENCE: the exact sequence of roundings of the reference's
@@ -513,7 +545,8 @@ using RngFor = XorwowT<IKPSO_ISSUE_SHL1_ADD != 0 && !(TERMS & kTermColliders)>;
 // this topology and term set: chains that run 4 waves per SIMD, no collider term
 // (whose contact decisions the tests compare across kernels bit for bit).
 template <class Topo, int MODE, int TERMS>
-constexpr bool kHwTrig = IKPSO_SINCOS_HW && MODE == IKPSO_ARITH_FAST && !(TERMS & kTermColliders) && Topo::D <= 30;
+constexpr bool kHwTrig = IKPSO_SINCOS_HW && MODE == IKPSO_ARITH_FAST && !(TERMS & kTermColliders) &&
+                        Topo::D <= IKPSO_HW_TRIG_MAX_D;
 
 // Which kernel builds honour ChainConsts::free_mask (the host routes masked
 // chains to them; the folded chain has no locked angles).
@@ -538,17 +571,43 @@ struct FitnessAcc {
 
     // Node k (1..J) with its three Euler angles, its three rest angles and (for
     // effectors) its target; nodes must come in index order.
+    // column-wise composition unless only the leaf's position is consumed
+    __device__ __forceinline__ static constexpr bool seq(int k)
+    {
+        return !Topo::kGeneric && (!Topo::leaf(k) || (TERMS & kTermColliders));
+    }
+
     __device__ __forceinline__ void node(const ChainConsts<J>& cc, int k, float a, float b, float c,
                                          const float* rest3, const float* tgt3, float* node_pos)
     {
-#pragma clang fp contract(off)
         const int pk = Topo::kGeneric ? cc.parent[k] : Topo::parent(k);
-        // column-wise composition unless only the leaf's position is consumed
         constexpr bool HW = kHwTrig<Topo, MODE, TERMS>;
-        if (!Topo::kGeneric && (!Topo::leaf(k) || (TERMS & kTermColliders)))
+        if (seq(k))
             F[k] = child_frame<MODE, true, HW>(F[pk], a, b, c, cc.len[k]);
         else
             F[k] = child_frame<MODE, false, HW>(F[pk], a, b, c, cc.len[k]);
+        terms(cc, k, a, b, c, rest3, tgt3, node_pos);
+    }
+
+    // FAST, with the node's sines and cosines computed ahead (node_trig).
+    __device__ __forceinline__ void node_trig(const ChainConsts<J>& cc, int k, const float* ang, const NodeTrig<3>& t,
+                                              const float* rest3, const float* tgt3, float* node_pos)
+    {
+        static_assert(MODE == IKPSO_ARITH_FAST, "precomputed sin/cos: FAST arithmetic");
+        const int pk = Topo::kGeneric ? cc.parent[k] : Topo::parent(k);
+        if (seq(k) && IKPSO_FK_SEQ)
+            F[k] = child_frame_fast_seq_sc(F[pk], t.s[0], t.c[0], t.s[1], t.c[1], t.s[2], t.c[2], cc.len[k]);
+        else
+            F[k] = child_frame_fast_sc(F[pk], t.s[0], t.c[0], t.s[1], t.c[1], t.s[2], t.c[2], cc.len[k]);
+        terms(cc, k, ang[0], ang[1], ang[2], rest3, tgt3, node_pos);
+    }
+
+    // The fitness terms of node k once its frame F[k] is known.
+    __device__ __forceinline__ void terms(const ChainConsts<J>& cc, int k, float a, float b, float c,
+                                          const float* rest3, const float* tgt3, float* node_pos)
+    {
+#pragma clang fp contract(off)
+        const int pk = Topo::kGeneric ? cc.parent[k] : Topo::parent(k);
         const float dx = rest3[0] - a, dy = rest3[1] - b, dz = rest3[2] - c;
         if constexpr (MODE == IKPSO_ARITH_REFERENCE) {
             rot_diff = rot_diff + ((dx * dx + dy * dy) + dz * dz);
@@ -652,6 +711,11 @@ struct FitnessAccDH {
     {
         float st, ct;
         sincos_fast<HW>(t, &st, &ct);
+        advance_sc(k, st, ct);
+    }
+
+    __device__ __forceinline__ void advance_sc(int k, float st, float ct)
+    {
         const float* C = dhc + 12 * (k - 1);
         float m00, m01, m02, m10, m11, m12, m20, m21, m22;
         if (k == 1) {
@@ -693,8 +757,20 @@ struct FitnessAccDH {
     __device__ __forceinline__ void node(const ChainConsts<J>& cc, int k, const float* ang, const float* rest,
                                          const float* tgt3, float* node_pos)
     {
-        const float t = ang[0];
-        advance(k, t);
+        advance(k, ang[0]);
+        terms(cc, k, ang[0], rest, tgt3, node_pos);
+    }
+
+    __device__ __forceinline__ void node_trig(const ChainConsts<J>& cc, int k, const float* ang, const NodeTrig<1>& t,
+                                              const float* rest, const float* tgt3, float* node_pos)
+    {
+        advance_sc(k, t.s[0], t.c[0]);
+        terms(cc, k, ang[0], rest, tgt3, node_pos);
+    }
+
+    __device__ __forceinline__ void terms(const ChainConsts<J>& cc, int k, float t, const float* rest,
+                                          const float* tgt3, float* node_pos)
+    {
         const float dt = rest[0] - t;
         rot_diff = rot_diff + dt * dt;
         if (penalty) {

@@ -22,6 +22,12 @@
 #ifndef IKPSO_DH_NODE_BARRIER
 #define IKPSO_DH_NODE_BARRIER 0
 #endif
+// Software-pipelined FAST iteration (swarm_step_ahead) for chains of up to this
+// many dimensions: the 4-wave kernels (config 3: -4 % kernel time).  The 2-wave
+// D = 60 kernel spills the extra live node under it (3x slower), so not there.
+#ifndef IKPSO_TRIG_AHEAD_MAX_D
+#define IKPSO_TRIG_AHEAD_MAX_D 30
+#endif
 
 namespace ikpso {
 
@@ -35,6 +41,61 @@ namespace ikpso {
 // reference's update-all-then-evaluate values in the same order.  The
 // node's LDS operands (local best, global best, rest pose, target) are
 // loaded one node ahead so their latency hides under the previous node.
+// simulateParticlesKernel for node k's A angles (draws r1, r2, r3 per
+// dimension, in dimension order; then the clamp).
+template <class Topo, int MODE, int TERMS, int BLOCK, class Rng>
+__device__ __forceinline__ void update_node(const ChainConsts<Topo::J>& cc, const SwarmShared<Topo>& sh,
+                                            const float* s_pb, int tid, int k, float (&x)[Topo::D],
+                                            float (&v)[Topo::D], const PsoCoef& coef, Rng& rng)
+{
+    constexpr int A = Topo::A;
+#pragma unroll
+    for (int ax = 0; ax < A; ++ax) {
+        const int d = A * (k - 1) + ax;
+        if (kMasked<Topo, TERMS> && !dim_free(cc, d)) continue;  // locked: stays at rest
+        pso_update<MODE>(x[d], v[d], s_pb[d * BLOCK + tid], sh.g[d], coef, rng);
+        if constexpr (TERMS & kTermUniformBounds)
+            x[d] = clamp_mode<MODE>(x[d], cc.lo[0], cc.hi[0]);
+        else
+            x[d] = clamp_mode<MODE>(x[d], sh.lo[d], sh.hi[d]);
+    }
+}
+
+// FAST: the same iteration software-pipelined by one node -- block k updates
+// node k+1's angles and evaluates their sines and cosines while it folds node k
+// into the FK, so the transcendental (or polynomial) latency of one node hides
+// under another node's FK.  The draws keep dimension order.
+template <class Topo, int MODE, int TERMS, int BLOCK, class Rng>
+__device__ __forceinline__ float swarm_step_ahead(const ChainConsts<Topo::J>& cc, SwarmShared<Topo>& sh,
+                                                  float* s_pb, int tid, float (&x)[Topo::D], float (&v)[Topo::D],
+                                                  const PsoCoef& coef, Rng& rng)
+{
+    constexpr int J = Topo::J, A = Topo::A;
+    constexpr bool HW = kHwTrig<Topo, MODE, TERMS>;
+    FitnessFor<Topo, MODE, TERMS> acc(cc, sh.dh);
+    update_node<Topo, MODE, TERMS, BLOCK>(cc, sh, s_pb, tid, 1, x, v, coef, rng);
+    NodeTrig<A> cur = node_trig<HW, A>(x);
+#pragma unroll
+    for (int k = 1; k <= J; ++k) {
+        NodeTrig<A> nxt = cur;
+        if (k < J) {
+            update_node<Topo, MODE, TERMS, BLOCK>(cc, sh, s_pb, tid, k + 1, x, v, coef, rng);
+            nxt = node_trig<HW, A>(x + A * k);
+        }
+        float rest[A], tgt[3];
+#pragma unroll
+        for (int ax = 0; ax < A; ++ax) rest[ax] = sh.rest[A * (k - 1) + ax];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) tgt[c] = Topo::effector(k) ? sh.tgt[3 * (k - 1) + c] : 0.0f;
+        acc.node_trig(cc, k, x + A * (k - 1), cur, rest, tgt, nullptr);
+        cur = nxt;
+#if !IKPSO_RES_NO_NODE_BARRIER
+        if (!Topo::kDH || IKPSO_DH_NODE_BARRIER) __builtin_amdgcn_sched_barrier(0);
+#endif
+    }
+    return acc.finish(cc);
+}
+
 // Masked chains (kMasked builds): a locked dimension takes no draws and keeps
 // its rest value, as in the oracle's masked restatement.
 template <class Topo, int MODE, int TERMS, int BLOCK, class Rng>
@@ -44,6 +105,16 @@ __device__ __forceinline__ void swarm_step(const ChainConsts<Topo::J>& cc, Swarm
 {
     constexpr int J = Topo::J, A = Topo::A, D = Topo::D;
     constexpr bool MASK = kMasked<Topo, TERMS>;
+    if constexpr (MODE == IKPSO_ARITH_FAST && Topo::D <= IKPSO_TRIG_AHEAD_MAX_D) {
+        // updateLocalBests (src/kernel.cu:202-221): strict improvement
+        const float f = swarm_step_ahead<Topo, MODE, TERMS, BLOCK>(cc, sh, s_pb, tid, x, v, coef, rng);
+        if (f < pbf) {
+            pbf = f;
+#pragma unroll
+            for (int d = 0; d < D; ++d) s_pb[d * BLOCK + tid] = x[d];
+        }
+        return;
+    }
     FitnessFor<Topo, MODE, TERMS> acc(cc, sh.dh);
     float npb[A], ng[A], nrest[A], ntgt[3];
 #pragma unroll

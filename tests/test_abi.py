@@ -112,3 +112,27 @@ def test_product_has_no_cpu_fallback():
             "from ikpso import _abi\ntry:\n _abi.load()\nexcept FileNotFoundError:\n print('LOUD')" % str(pkg))
     out = subprocess.run(["python", "-c", code], capture_output=True, text=True)
     assert "LOUD" in out.stdout
+
+
+def test_compat_refuses_other_dof(tmp_path):
+    """A caller compiled with another DEGREES_OF_FREEDOM than the library gets
+    hipErrorInvalidConfiguration from calculatePSO (no device work), one built
+    with the library's value reaches the argument checks (hipErrorInvalidValue
+    for the null buffers below)."""
+    src = tmp_path / "caller.cpp"
+    src.write_text(
+        '#include "ikpso_compat.h"\n#include <cstdio>\n'
+        "int main() {\n"
+        "  PSOConfig p(0.5f, 0.5f, 1.25f, 1); FitnessConfig f;\n"
+        "  hipError_t e = calculatePSO(nullptr, nullptr, nullptr, nullptr, 0, nullptr, p, f, nullptr, nullptr, 0);\n"
+        '  std::printf("%d\\n", (int)e); return 0; }\n')
+    lib = ROOT / "inverse-kinematics-pso-research_amd" / "ikpso" / "_lib"
+    codes = {}
+    for dof in (21, 24):
+        exe = tmp_path / f"caller{dof}"
+        subprocess.run(["/opt/rocm/bin/hipcc", f"-DDEGREES_OF_FREEDOM={dof}", "-I", str(ROOT / "include"), str(src),
+                        "-o", str(exe), f"-L{lib}", "-likpso", f"-Wl,-rpath,{lib}"], check=True,
+                       capture_output=True)
+        codes[dof] = int(subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout)
+    assert codes[21] == 1      # hipErrorInvalidValue: argument checks
+    assert codes[24] == 9      # hipErrorInvalidConfiguration: D mismatch

@@ -35,15 +35,18 @@ for pas in ("valu", "fetch", "write", "cycles"):
     big = max((k for k in agg if pat in k[1]), key=lambda k: int(k[2]))
     counters[pas] = agg[big]
 valu = counters["valu"]["SQ_INSTS_VALU"] * 64 / upd
+trans = counters["valu"].get("SQ_INSTS_VALU_TRANS_F32")  # v_sin/v_cos/...: 4 issue slots each on gfx950
+trans = None if trans is None else trans * 64 / upd
 fb = counters["fetch"]["FETCH_SIZE"] * 1024 * 2  # KiB; x2: gfx950 FETCH_SIZE counts half a streaming read
 wb = counters["write"]["WRITE_SIZE"] * 1024
 cyc = counters["cycles"]
 res = {
     "valu_lane_instr_per_update": round(valu, 1),
+    "trans_lane_instr_per_update": None if trans is None else round(trans, 1),
     "hbm_bytes_per_update": round((fb + wb) / upd, 4),
     "wave_cycle_split": {k: round(cyc[k] / cyc["SQ_WAVE_CYCLES"], 3)
                          for k in ("SQ_ACTIVE_INST_ANY", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY")},
-    "source": f"rocprofv3 --pmc SQ_INSTS_VALU / FETCH_SIZE / WRITE_SIZE / cycles (separate passes) of {pat}, "
+    "source": f"rocprofv3 --pmc SQ_INSTS_VALU (+ SQ_INSTS_VALU_TRANS_F32) / FETCH_SIZE / WRITE_SIZE / cycles (separate passes) of {pat}, "
               f"{upd} particle-updates per dispatch; profiles/{rnd}/{name}_pmc_*.csv. lane-instr/update = "
               "SQ_INSTS_VALU * 64 / updates; bytes = (2*FETCH_SIZE + WRITE_SIZE) KiB*1024 / updates",
     "fetch_bytes": fb, "write_bytes": wb, "updates": upd,
