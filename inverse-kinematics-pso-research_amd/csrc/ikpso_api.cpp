@@ -523,6 +523,7 @@ hipError_t carve_coop(SwarmIO& io, void* ws, int G, int NG, int block, int D, hi
     io.coop_counter = cv.take<uint32_t>((size_t)NG * kCoopCounterStride);
     io.coop_error = cv.take<int32_t>(1);
     io.coop_slots = cv.take<float>((size_t)NG * 2 * G * kCoopSlot(D));
+    io.coop_pbest = coop_global_pbest(D) ? cv.take<float>((size_t)NG * G * D * block) : nullptr;
     io.coop_g = G;
     io.coop_ng = NG;
     io.coop_block = block;
@@ -715,7 +716,7 @@ ikpso_status ikpso_calculate_pso(float* particles, const float* positions, float
     const size_t snap = ((sizeof(ikpso_rng_state) * (size_t)size + 255) & ~size_t(255));
     const size_t ws = family_run == IKPSO_KERNEL_STREAMING ? sws
                       : family_run == IKPSO_KERNEL_COOP
-                          ? ((coop_workspace_bytes(cng, cg, D) + 255) & ~size_t(255)) + snap + sws
+                          ? ((coop_workspace_bytes(cng, cg, D, cblk) + 255) & ~size_t(255)) + snap + sws
                           : 0;
     float* dres = nullptr;
     st = scratch(((head + 255) & ~size_t(255)) + ws, &dres);
@@ -744,7 +745,7 @@ ikpso_status ikpso_calculate_pso(float* particles, const float* positions, float
         io.num_swarms = 1;
         char* wsb = reinterpret_cast<char*>(dres) + ((head + 255) & ~size_t(255));
         ikpso_rng_state* rsnap =
-            reinterpret_cast<ikpso_rng_state*>(wsb + ((coop_workspace_bytes(cng, cg, D) + 255) & ~size_t(255)));
+            reinterpret_cast<ikpso_rng_state*>(wsb + ((coop_workspace_bytes(cng, cg, D, cblk) + 255) & ~size_t(255)));
         IKPSO_HIP(hipMemcpyAsync(rsnap, randoms, sizeof(ikpso_rng_state) * (size_t)size, hipMemcpyDeviceToDevice, s));
         IKPSO_HIP(carve_coop(io, wsb, cg, cng, cblk, D, s));
         IKPSO_HIP(launch_coop(ch, mode, io, s));
@@ -940,7 +941,7 @@ ikpso_status ikpso_solve_batch(ikpso_solver* s, const float* targets, const floa
         int G, NG, T;
         if (!coop_plan(ch, s->mode, s->P, num_swarms, s->requested == IKPSO_KERNEL_AUTO, &G, &NG, &T))
             return IKPSO_ERR_UNSUPPORTED;
-        ikpso_status st = grow(&s->ws, &s->ws_bytes, coop_workspace_bytes(NG, G, D));
+        ikpso_status st = grow(&s->ws, &s->ws_bytes, coop_workspace_bytes(NG, G, D, T));
         if (st != IKPSO_OK) return st;
         // snapshot of the generator states the launch starts from (48 B per
         // particle, one D2D copy): the fallback re-runs the batch from it

@@ -72,8 +72,42 @@ struct CoopShared {
 // chunks, reduce; returns the group-wide minimum key of this exchange (uniform)
 // and leaves the winner's local best in sh.g when it improves on `gkey` (or
 // always when `force`).  Called by every wave; wave 0 does the global work.
-template <class Topo, int BLOCK>
-__device__ __forceinline__ void coop_exchange(SwarmShared<Topo>& sh, CoopShared<Topo::J>& cs, const float* s_pb,
+// One chunk's local-best plane [d][lane] in global memory (coop_global_pbest):
+// a buffer resource, so an access costs one VGPR offset (the lane) and an SGPR
+// offset (the dimension) instead of a 64-bit address per dimension.
+struct PbPlane {
+    __amdgpu_buffer_rsrc_t rsrc;
+    uint32_t voff;
+    __device__ __forceinline__ PbPlane(float* base, int D, int block, int lane)
+        : rsrc(__builtin_amdgcn_make_buffer_rsrc(base, 0, D * block * 4, 0x00020000)), voff((uint32_t)lane * 4u)
+    {
+    }
+    template <int BLOCK>
+    __device__ __forceinline__ float ld(int d) const
+    {
+        return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsrc, (int)voff, d * BLOCK * 4, 0));
+    }
+    template <int BLOCK>
+    __device__ __forceinline__ void st(int d, float v) const
+    {
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rsrc, (int)voff, d * BLOCK * 4, 0);
+    }
+};
+
+// The winner's local best: from the LDS array [d][lane] or the global plane.
+template <int BLOCK>
+__device__ __forceinline__ float local_best(const float* s_pb, int d, int lane)
+{
+    return s_pb[d * BLOCK + lane];
+}
+template <int BLOCK>
+__device__ __forceinline__ float local_best(const PbPlane& pb, int d, int lane)
+{
+    return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(pb.rsrc, lane * 4, d * BLOCK * 4, 0));
+}
+
+template <class Topo, int BLOCK, class PB>
+__device__ __forceinline__ void coop_exchange(SwarmShared<Topo>& sh, CoopShared<Topo::J>& cs, const PB& s_pb,
                                               uint32_t local_key, int32_t* error, uint32_t spin_limit, bool force)
 {
     constexpr int D = Topo::D;
@@ -91,7 +125,7 @@ __device__ __forceinline__ void coop_exchange(SwarmShared<Topo>& sh, CoopShared<
         float* base = slots + (size_t)(e & 1) * G * SLOT;
         float* mine = base + (size_t)member * SLOT;
         // lanes 0..D-1: the winner's local best; lane D: key; lane D+1: global index
-        if (lane < D) st_sc1(mine + 2 + lane, s_pb[lane * BLOCK + lidx]);
+        if (lane < D) st_sc1(mine + 2 + lane, local_best<BLOCK>(s_pb, lane, lidx));
         if (lane == D) st_sc1(mine, __uint_as_float(lmin));
         if (lane == D + 1) st_sc1(mine + 1, __int_as_float(member * BLOCK + lidx));
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -133,6 +167,90 @@ __device__ __forceinline__ void coop_exchange(SwarmShared<Topo>& sh, CoopShared<
     __syncthreads();
 }
 
+#ifndef IKPSO_PBG_HW
+#define IKPSO_PBG_HW 1        // FAST sin/cos on the transcendental unit in the long-chain build
+#endif
+#ifndef IKPSO_PBG_AHEAD
+#define IKPSO_PBG_AHEAD 2     // nodes of local bests loaded ahead of their use
+#endif
+#ifndef IKPSO_PBG_V_AHEAD
+#define IKPSO_PBG_V_AHEAD 1   // nodes of velocities read from LDS ahead of their use
+#endif
+
+// One PSO iteration of the long-chain build: positions in VGPRs, velocities in
+// LDS (s_v[d][lane]), local bests in the chunk's global plane, loaded
+// IKPSO_PBG_AHEAD nodes ahead.  Same arithmetic and draw order as swarm_step.
+template <class Topo, int MODE, int TERMS, int BLOCK, class Rng>
+__device__ __forceinline__ void swarm_step_pbg(const ChainConsts<Topo::J>& cc, SwarmShared<Topo>& sh, float* s_v,
+                                               const PbPlane& pb, int tid, float (&x)[Topo::D], float& pbf,
+                                               const PsoCoef& coef, Rng& rng)
+{
+    constexpr int J = Topo::J, A = Topo::A, D = Topo::D;
+    constexpr bool MASK = kMasked<Topo, TERMS>;
+    constexpr bool HW = IKPSO_PBG_HW && IKPSO_SINCOS_HW && MODE == IKPSO_ARITH_FAST && !(TERMS & kTermColliders);
+    constexpr int AH = (IKPSO_PBG_AHEAD < J) ? IKPSO_PBG_AHEAD : J;
+    constexpr int VH = (IKPSO_PBG_V_AHEAD < J) ? IKPSO_PBG_V_AHEAD : J;
+    FitnessFor<Topo, MODE, TERMS> acc(cc, sh.dh);
+    float ring[AH + 1][A], vring[VH + 1][A];
+#pragma unroll
+    for (int n = 0; n < AH; ++n)
+#pragma unroll
+        for (int ax = 0; ax < A; ++ax) ring[n][ax] = pb.template ld<BLOCK>(A * n + ax);
+#pragma unroll
+    for (int n = 0; n < VH; ++n)
+#pragma unroll
+        for (int ax = 0; ax < A; ++ax) vring[n][ax] = s_v[(A * n + ax) * BLOCK + tid];
+#pragma unroll
+    for (int k = 1; k <= J; ++k) {
+        const int cs = (k - 1) % (AH + 1), cv = (k - 1) % (VH + 1);
+        float cpb[A], cvel[A];
+#pragma unroll
+        for (int ax = 0; ax < A; ++ax) {
+            cpb[ax] = ring[cs][ax];
+            cvel[ax] = vring[cv][ax];
+        }
+        if (k - 1 + AH < J) {
+            const int nn = k - 1 + AH, ns = nn % (AH + 1);
+#pragma unroll
+            for (int ax = 0; ax < A; ++ax) ring[ns][ax] = pb.template ld<BLOCK>(A * nn + ax);
+        }
+        if (k - 1 + VH < J) {
+            const int nn = k - 1 + VH, ns = nn % (VH + 1);
+#pragma unroll
+            for (int ax = 0; ax < A; ++ax) vring[ns][ax] = s_v[(A * nn + ax) * BLOCK + tid];
+        }
+#pragma unroll
+        for (int ax = 0; ax < A; ++ax) {
+            const int d = A * (k - 1) + ax;
+            if (MASK && !dim_free(cc, d)) continue;  // locked: stays at rest
+            float vv = cvel[ax];
+            pso_update<MODE>(x[d], vv, cpb[ax], sh.g[d], coef, rng);
+            s_v[d * BLOCK + tid] = vv;
+            if constexpr (TERMS & kTermUniformBounds)
+                x[d] = clamp_mode<MODE>(x[d], cc.lo[0], cc.hi[0]);
+            else
+                x[d] = clamp_mode<MODE>(x[d], sh.lo[d], sh.hi[d]);
+        }
+        float rest[A], tgt[3];
+#pragma unroll
+        for (int ax = 0; ax < A; ++ax) rest[ax] = sh.rest[A * (k - 1) + ax];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) tgt[c] = Topo::effector(k) ? sh.tgt[3 * (k - 1) + c] : 0.0f;
+        if constexpr (MODE == IKPSO_ARITH_FAST)
+            acc.node_trig(cc, k, x + A * (k - 1), node_trig<HW, A>(x + A * (k - 1)), rest, tgt, nullptr);
+        else
+            acc.node(cc, k, x + A * (k - 1), rest, tgt, nullptr);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    // updateLocalBests (src/kernel.cu:202-221): strict improvement
+    const float f = acc.finish(cc);
+    if (f < pbf) {
+        pbf = f;
+#pragma unroll
+        for (int d = 0; d < D; ++d) pb.template st<BLOCK>(d, x[d]);
+    }
+}
+
 // BLOCK: kCoopThreads<D>() (throughput: fill each CU), or kCoopLatencyThreads
 // for a few swarms (latency: one wave per SIMD on 4x more CUs).
 template <class Topo, int MODE, int TERMS, int BLOCK>
@@ -141,15 +259,18 @@ __global__ void __launch_bounds__(BLOCK, (BLOCK >= 256 ? BLOCK / 256 : 1))
 {
     constexpr int J = Topo::J;
     constexpr int D = Topo::D;
+    constexpr bool PBG = coop_global_pbest(D);
     const int tid = threadIdx.x;
     const int P = io.P;
 
     __shared__ SwarmShared<Topo> sh;
     __shared__ CoopShared<J> cs;
-    // local bests [d][lane]; padded to > 80 KiB so a CU never holds two
+    // local bests [d][lane] (PBG: the velocities; the local bests are in the
+    // chunk's global plane); padded to > 80 KiB so a CU never holds two
     // workgroups (the launch geometry assumes one per CU)
     constexpr int kPb = (D * BLOCK * 4 > 82 * 1024) ? D * BLOCK : 82 * 1024 / 4;
     __shared__ float s_pb[kPb];
+    const PbPlane pbg(PBG ? io.coop_pbest + (size_t)blockIdx.x * D * BLOCK : nullptr, D, BLOCK, tid);
     if (tid == 0) {
         // XCD-aware group membership: workgroups b, b+8, b+16, ... share an XCD
         const int G = io.coop_g;
@@ -181,18 +302,39 @@ __global__ void __launch_bounds__(BLOCK, (BLOCK >= 256 ? BLOCK / 256 : 1))
         __syncthreads();
 
         // initParticlesKernel + initLocalBests (src/kernel.cu:191-266)
-        float x[D], v[D];
-        init_particle<Topo, TERMS, BLOCK>(cc, sh, s_pb, tid, x, v, rng);
+        float x[D], v[PBG ? 1 : D];
+        if constexpr (PBG) {
+#pragma unroll
+            for (int d = 0; d < D; ++d) {
+                x[d] = sh.rest[d];
+                const bool locked = kMasked<Topo, TERMS> && !dim_free(cc, d);
+                s_pb[d * BLOCK + tid] = locked ? 0.0f : __builtin_fmaf(rng.uniform(), 2.0f, -1.0f);
+                pbg.template st<BLOCK>(d, x[d]);
+            }
+        } else {
+            init_particle<Topo, TERMS, BLOCK>(cc, sh, s_pb, tid, x, v, rng);
+        }
         float pbf = fitness<Topo, MODE, TERMS>(cc, x, sh.rest, sh.tgt, nullptr, sh.dh);
         // swarm argmin + unconditional first global-best copy (src/kernel.cu:297-304)
-        coop_exchange<Topo, BLOCK>(sh, cs, s_pb, i < P ? ordered_key(pbf) : 0xFFFFFFFFu, io.coop_error, io.coop_spin_limit, true);
+        const uint32_t key0 = i < P ? ordered_key(pbf) : 0xFFFFFFFFu;
+        if constexpr (PBG)
+            coop_exchange<Topo, BLOCK>(sh, cs, pbg, key0, io.coop_error, io.coop_spin_limit, true);
+        else
+            coop_exchange<Topo, BLOCK>(sh, cs, s_pb, key0, io.coop_error, io.coop_spin_limit, true);
 
         for (int it = 0; it < io.iterations; ++it) {
             compiler_fence();
             if (cs.abort) break;
-            swarm_step<Topo, MODE, TERMS, BLOCK>(cc, sh, s_pb, tid, x, v, pbf, coef, rng);
+            if constexpr (PBG)
+                swarm_step_pbg<Topo, MODE, TERMS, BLOCK>(cc, sh, s_pb, pbg, tid, x, pbf, coef, rng);
+            else
+                swarm_step<Topo, MODE, TERMS, BLOCK>(cc, sh, s_pb, tid, x, v, pbf, coef, rng);
             const bool act = cs.member * BLOCK + tid < P;
-            coop_exchange<Topo, BLOCK>(sh, cs, s_pb, act ? ordered_key(pbf) : 0xFFFFFFFFu, io.coop_error, io.coop_spin_limit, false);
+            const uint32_t key = act ? ordered_key(pbf) : 0xFFFFFFFFu;
+            if constexpr (PBG)
+                coop_exchange<Topo, BLOCK>(sh, cs, pbg, key, io.coop_error, io.coop_spin_limit, false);
+            else
+                coop_exchange<Topo, BLOCK>(sh, cs, s_pb, key, io.coop_error, io.coop_spin_limit, false);
         }
 
         compiler_fence();
@@ -217,8 +359,13 @@ __global__ void __launch_bounds__(BLOCK, (BLOCK >= 256 ? BLOCK / 256 : 1))
 #pragma unroll
                 for (int d = 0; d < D; ++d) {
                     base[(int64_t)d * P + ii] = x[d];
-                    base[(int64_t)(D + d) * P + ii] = v[d];
-                    base[(int64_t)(2 * D + d) * P + ii] = s_pb[d * BLOCK + tid];
+                    if constexpr (PBG) {
+                        base[(int64_t)(D + d) * P + ii] = s_pb[d * BLOCK + tid];
+                        base[(int64_t)(2 * D + d) * P + ii] = pbg.template ld<BLOCK>(d);
+                    } else {
+                        base[(int64_t)(D + d) * P + ii] = v[d];
+                        base[(int64_t)(2 * D + d) * P + ii] = s_pb[d * BLOCK + tid];
+                    }
                 }
             }
             if (io.dump_bests) io.dump_bests[bb * P + ii] = pbf;

@@ -91,6 +91,18 @@ __host__ __device__ constexpr int kCoopThreads()
     return D <= 30 ? 1024 : 512;
 }
 
+// Experiment (off): for long chains (D > 30: 512-lane chunks, x and v take 120
+// VGPRs at D = 60) keep each chunk's local bests in a global plane (L2-resident:
+// 120 KiB per CU) and the velocities in LDS, so only the positions occupy VGPRs.
+// Measured on config 5 (2048 swarms x 4096 x 100): no spills in the iteration
+// loop and 3958 issue slots per update instead of 4651, yet 119-122 ms against
+// 97.6 ms -- the LDS velocity round trip and the global loads cost more than the
+// registers they free at 2 waves per SIMD.
+#ifndef IKPSO_COOP_PBG
+#define IKPSO_COOP_PBG 0
+#endif
+__host__ __device__ constexpr bool coop_global_pbest(int D) { return IKPSO_COOP_PBG && D > 30; }
+
 // Published record of one chunk: key, global particle index, D floats, padded
 // to a 64-B multiple.
 __host__ __device__ constexpr int kCoopSlot(int D) { return ((D + 2 + 15) / 16) * 16; }
@@ -161,7 +173,7 @@ struct CoopGeometry {
     bool latency_variant = false;  // a kCoopLatencyThreads build exists for this chain
 };
 bool coop_geometry(const ChainHost& ch, int mode, CoopGeometry* g);
-size_t coop_workspace_bytes(int ng, int G, int D);
+size_t coop_workspace_bytes(int ng, int G, int D, int block);
 int resident_max_threads(const ChainHost& ch);
 bool chain_supported(const ChainHost& ch);
 std::string kernel_name(const ChainHost& ch, int family);  // IKPSO_KERNEL_*

@@ -151,10 +151,11 @@ bool coop_geometry(const ChainHost& ch, int mode, CoopGeometry* g)
     return true;
 }
 
-size_t coop_workspace_bytes(int ng, int G, int D)
+size_t coop_workspace_bytes(int ng, int G, int D, int block)
 {
+    const size_t pbg = coop_global_pbest(D) ? sizeof(float) * (size_t)ng * G * D * block + 256 : 0;
     return sizeof(uint32_t) * (size_t)ng * kCoopCounterStride + sizeof(float) * (size_t)ng * 2 * G * kCoopSlot(D) +
-           256 + 3 * 256;
+           256 + 3 * 256 + pbg;
 }
 
 hipError_t launch_stream(const ChainHost& ch, int mode, const StreamIO& io, int iterations, hipStream_t stream)
