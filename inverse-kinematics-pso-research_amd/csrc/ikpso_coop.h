@@ -115,6 +115,18 @@ __device__ __forceinline__ void coop_exchange(SwarmShared<Topo>& sh, CoopShared<
     static_assert(D + 2 <= 64, "wave 0 publishes the record in one store instruction");
     int lidx;
     const uint32_t lmin = swarm_argmin(sh, 0, local_key, &lidx);  // one workgroup barrier inside
+#if IKPSO_COOP_NO_EXCHANGE  // timing-only ablation: every chunk its own swarm (no cross-CU hand-off)
+    if (wave_id() == 0) {
+        const int lane = lane_id_here();
+        if (force || lmin < cs.gkey) {
+            if (lane < D) sh.g[lane] = local_best<BLOCK>(s_pb, lane, lidx);
+            if (lane == 0) cs.gkey = lmin;
+        }
+        (void)error, (void)spin_limit, (void)SLOT;
+    }
+    __syncthreads();
+    return;
+#endif
     if (wave_id() == 0) {
         compiler_fence();
         const int G = cs.G, member = cs.member;
@@ -167,6 +179,9 @@ __device__ __forceinline__ void coop_exchange(SwarmShared<Topo>& sh, CoopShared<
     __syncthreads();
 }
 
+#ifndef IKPSO_COOP_SHL1_ADD
+#define IKPSO_COOP_SHL1_ADD 0  // the add-for-shift generator form in the throughput build too
+#endif
 #ifndef IKPSO_PBG_HW
 #define IKPSO_PBG_HW 1        // FAST sin/cos on the transcendental unit in the long-chain build
 #endif
@@ -190,7 +205,7 @@ __device__ __forceinline__ void swarm_step_pbg(const ChainConsts<Topo::J>& cc, S
     constexpr bool HW = IKPSO_PBG_HW && IKPSO_SINCOS_HW && MODE == IKPSO_ARITH_FAST && !(TERMS & kTermColliders);
     constexpr int AH = (IKPSO_PBG_AHEAD < J) ? IKPSO_PBG_AHEAD : J;
     constexpr int VH = (IKPSO_PBG_V_AHEAD < J) ? IKPSO_PBG_V_AHEAD : J;
-    FitnessFor<Topo, MODE, TERMS> acc(cc, sh.dh);
+    FitnessFor<Topo, MODE, TERMS> acc(cc, sh.dh, sh.soft);
     float ring[AH + 1][A], vring[VH + 1][A];
 #pragma unroll
     for (int n = 0; n < AH; ++n)
@@ -263,13 +278,14 @@ __global__ void __launch_bounds__(BLOCK, (BLOCK >= 256 ? BLOCK / 256 : 1))
     const int tid = threadIdx.x;
     const int P = io.P;
 
-    __shared__ SwarmShared<Topo> sh;
-    __shared__ CoopShared<J> cs;
     // local bests [d][lane] (PBG: the velocities; the local bests are in the
     // chunk's global plane); padded to > 80 KiB so a CU never holds two
     // workgroups (the launch geometry assumes one per CU)
     constexpr int kPb = (D * BLOCK * 4 > 82 * 1024) ? D * BLOCK : 82 * 1024 / 4;
-    __shared__ float s_pb[kPb];
+    __shared__ SwarmLds<Topo, kPb, CoopShared<J>> lds;
+    SwarmShared<Topo>& sh = lds.sh;
+    CoopShared<J>& cs = lds.extra;
+    float* const s_pb = lds.pb;
     const PbPlane pbg(PBG ? io.coop_pbest + (size_t)blockIdx.x * D * BLOCK : nullptr, D, BLOCK, tid);
     if (tid == 0) {
         // XCD-aware group membership: workgroups b, b+8, b+16, ... share an XCD
@@ -295,7 +311,8 @@ __global__ void __launch_bounds__(BLOCK, (BLOCK >= 256 ? BLOCK / 256 : 1))
         stage_swarm_inputs<Topo>(cc, io.targets, io.start_pose, b, sh);
         // the add-for-shift issue form only in the latency variant (one wave per
         // SIMD, room to spare): in the 2-wave serial-20 kernel it cost 5 %
-        using Rng = XorwowT<(BLOCK == kCoopLatencyThreads) && std::is_same_v<RngFor<TERMS>, XorwowT<true>>>;
+        using Rng = XorwowT<(IKPSO_COOP_SHL1_ADD || BLOCK == kCoopLatencyThreads) &&
+                            std::is_same_v<RngFor<TERMS>, XorwowT<true>>>;
         Rng rng{0, 0, 0, 0, 0, 0};
         if (i < P) load_rng(rng, io.rng + b * P + i);
         if (tid == 0) cs.gkey = 0xFFFFFFFFu;
@@ -314,7 +331,7 @@ __global__ void __launch_bounds__(BLOCK, (BLOCK >= 256 ? BLOCK / 256 : 1))
         } else {
             init_particle<Topo, TERMS, BLOCK>(cc, sh, s_pb, tid, x, v, rng);
         }
-        float pbf = fitness<Topo, MODE, TERMS>(cc, x, sh.rest, sh.tgt, nullptr, sh.dh);
+        float pbf = fitness<Topo, MODE, TERMS>(cc, x, sh.rest, sh.tgt, nullptr, sh.dh, sh.soft);
         // swarm argmin + unconditional first global-best copy (src/kernel.cu:297-304)
         const uint32_t key0 = i < P ? ordered_key(pbf) : 0xFFFFFFFFu;
         if constexpr (PBG)

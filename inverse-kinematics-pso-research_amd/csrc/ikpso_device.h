@@ -50,7 +50,7 @@
 #define IKPSO_SINCOS_HW 1
 #endif
 #ifndef IKPSO_HW_TRIG_MAX_D
-#define IKPSO_HW_TRIG_MAX_D 30
+#define IKPSO_HW_TRIG_MAX_D 60
 #endif
 
 
@@ -559,11 +559,15 @@ template <class Topo, int MODE, int TERMS>
 struct FitnessAcc {
     static constexpr int J = Topo::J;
     Frame F[J + 1];
+    const float* soft;  // soft limits [lo 3J | hi 3J]: the swarm kernels' LDS copy, else aux in HBM
     float rot_diff, pos_diff, distance, pen;
     bool hit, posref, penalty;
 
-    __device__ __forceinline__ explicit FitnessAcc(const ChainConsts<J>& cc, const float* = nullptr)
-        : rot_diff(0.0f), pos_diff(0.0f), distance(0.0f), pen(0.0f), hit(false),
+    // soft_: the soft limits -- pass the swarm kernel's LDS copy (SwarmShared::soft)
+    // where there is one: a pointer that may be LDS or global is a flat pointer
+    __device__ __forceinline__ FitnessAcc(const ChainConsts<J>& cc, const float*, const float* soft_)
+        : soft(soft_), rot_diff(0.0f), pos_diff(0.0f), distance(0.0f), pen(0.0f),
+          hit(false),
           posref((TERMS & kTermPosRef) || ((TERMS & kTermRuntime) && cc.use_posref)),
           penalty((TERMS & kTermPenalty) || ((TERMS & kTermRuntime) && cc.use_penalty))
     {
@@ -640,7 +644,7 @@ struct FitnessAcc {
 #pragma unroll
             for (int ax = 0; ax < 3; ++ax) {
                 const int d = 3 * (k - 1) + ax;
-                const float slo = cc.aux[4 * J + d], shi = cc.aux[7 * J + d];
+                const float slo = soft[d], shi = soft[3 * J + d];
                 const float over = fmaxf(fmaxf(ang[ax] - shi, slo - ang[ax]), 0.0f);
                 pen = pen + over * over;
             }
@@ -692,14 +696,15 @@ struct FitnessAccDH {
     static constexpr bool HW = kHwTrig<Topo, MODE, TERMS>;
     static_assert(MODE == IKPSO_ARITH_FAST, "the folded chain is FAST arithmetic only");
     const float* dhc;
+    const float* soft;                                  // soft limits [lo 3J | hi 3J] (see FitnessAcc)
     float w00, w01, w02, w10, w11, w12, w20, w21, w22;  // current joint frame W_j
     float qx, qy, qz;                                   // position q_j
     float px, py, pz;                                   // tip (after joint J)
     float rot_diff, distance, pen;
     bool penalty;
 
-    __device__ __forceinline__ FitnessAccDH(const ChainConsts<J>& cc, const float* dh)
-        : dhc(dh), rot_diff(0.0f), distance(0.0f), pen(0.0f),
+    __device__ __forceinline__ FitnessAccDH(const ChainConsts<J>& cc, const float* dh, const float* soft_)
+        : dhc(dh), soft(soft_), rot_diff(0.0f), distance(0.0f), pen(0.0f),
           penalty((TERMS & kTermPenalty) || ((TERMS & kTermRuntime) && cc.use_penalty))
     {
         qx = dhc[12 * J + 0];
@@ -776,7 +781,7 @@ struct FitnessAccDH {
         rot_diff = rot_diff + dt * dt;
         if (penalty) {
             const int d = k - 1;
-            const float slo = cc.aux[4 * J + d], shi = cc.aux[7 * J + d];
+            const float slo = soft[d], shi = soft[3 * J + d];
             const float over = fmaxf(fmaxf(t - shi, slo - t), 0.0f);
             pen = pen + over * over;
         }
@@ -803,14 +808,15 @@ template <class Topo, int MODE, int TERMS>
 using FitnessFor =
     std::conditional_t<Topo::kDH, FitnessAccDH<Topo, MODE, TERMS>, FitnessAcc<Topo, MODE, TERMS>>;
 
-// x, rest: [D]; tgt: [3J] (per node); dhc: the folded chain's constants (TopoDH).
+// x, rest: [D]; tgt: [3J] (per node); dhc: the folded chain's constants (TopoDH);
+// soft: the soft limits [lo 3J | hi 3J] (SwarmShared::soft, or cc.aux + 4J).
 template <class Topo, int MODE, int TERMS>
 __device__ __forceinline__ float fitness(const ChainConsts<Topo::J>& cc, const float* x, const float* rest,
                                          const float* tgt, float* node_pos /* [3J] or nullptr */,
-                                         const float* dhc = nullptr)
+                                         const float* dhc, const float* soft)
 {
     constexpr int A = Topo::A;
-    FitnessFor<Topo, MODE, TERMS> acc(cc, dhc);
+    FitnessFor<Topo, MODE, TERMS> acc(cc, dhc, soft);
 #pragma unroll
     for (int k = 1; k <= Topo::J; ++k) {
         acc.node(cc, k, x + A * (k - 1), rest + A * (k - 1), tgt + 3 * (k - 1), node_pos);
@@ -832,7 +838,7 @@ __device__ __forceinline__ float residual(const ChainConsts<Topo::J>& cc, const 
 {
     constexpr int J = Topo::J;
     if constexpr (Topo::kDH) {
-        FitnessAccDH<Topo, MODE, TERMS> acc(cc, dhc);
+        FitnessAccDH<Topo, MODE, TERMS> acc(cc, dhc, cc.aux);  // (no penalty term here)
 #pragma unroll
         for (int k = 1; k <= J; ++k) acc.advance(k, x[k - 1]);
         const float dx = tgt[3 * (J - 1) + 0] - acc.px;
@@ -898,6 +904,14 @@ __device__ __forceinline__ void pso_update(float& x, float& v, float pb, float g
         v = __builtin_fmaf(a, v, __builtin_fmaf(b, pb - x, c * (g - x)));
         x += v;
     }
+}
+
+// FAST, with the dimension's three scaled uniforms drawn earlier (in the same
+// order): a = w*r1, b = c1*r2, c = c2*r3.
+__device__ __forceinline__ void pso_update_drawn(float& x, float& v, float pb, float g, float a, float b, float c)
+{
+    v = __builtin_fmaf(a, v, __builtin_fmaf(b, pb - x, c * (g - x)));
+    x += v;
 }
 
 // clamp (src/matrix_operations.cuh:187-190)

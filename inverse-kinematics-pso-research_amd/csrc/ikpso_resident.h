@@ -25,6 +25,12 @@
 // Software-pipelined FAST iteration (swarm_step_ahead) for chains of up to this
 // many dimensions: the 4-wave kernels (config 3: -4 % kernel time).  The 2-wave
 // D = 60 kernel spills the extra live node under it (3x slower), so not there.
+#ifndef IKPSO_NODE_BARRIER_EVERY
+#define IKPSO_NODE_BARRIER_EVERY 1  // long-chain step: scheduling region = this many nodes
+#endif
+#ifndef IKPSO_DRAWS_AHEAD
+#define IKPSO_DRAWS_AHEAD 0
+#endif
 #ifndef IKPSO_TRIG_AHEAD_MAX_D
 #define IKPSO_TRIG_AHEAD_MAX_D 30
 #endif
@@ -72,7 +78,7 @@ __device__ __forceinline__ float swarm_step_ahead(const ChainConsts<Topo::J>& cc
 {
     constexpr int J = Topo::J, A = Topo::A;
     constexpr bool HW = kHwTrig<Topo, MODE, TERMS>;
-    FitnessFor<Topo, MODE, TERMS> acc(cc, sh.dh);
+    FitnessFor<Topo, MODE, TERMS> acc(cc, sh.dh, sh.soft);
     update_node<Topo, MODE, TERMS, BLOCK>(cc, sh, s_pb, tid, 1, x, v, coef, rng);
     NodeTrig<A> cur = node_trig<HW, A>(x);
 #pragma unroll
@@ -115,7 +121,20 @@ __device__ __forceinline__ void swarm_step(const ChainConsts<Topo::J>& cc, Swarm
         }
         return;
     }
-    FitnessFor<Topo, MODE, TERMS> acc(cc, sh.dh);
+    FitnessFor<Topo, MODE, TERMS> acc(cc, sh.dh, sh.soft);
+    // FAST long chains: node k+1's draws are generated while node k is folded
+    // into the FK (integer work the scheduler can interleave with the float
+    // chain; the draw order is unchanged)
+    constexpr bool AHEAD = IKPSO_DRAWS_AHEAD && MODE == IKPSO_ARITH_FAST && !MASK;
+    float nd[A][3];
+    if constexpr (AHEAD) {
+#pragma unroll
+        for (int ax = 0; ax < A; ++ax) {
+            nd[ax][0] = rng.scaled(coef.wq, coef.wh);
+            nd[ax][1] = rng.scaled(coef.c1q, coef.c1h);
+            nd[ax][2] = rng.scaled(coef.c2q, coef.c2h);
+        }
+    }
     float npb[A], ng[A], nrest[A], ntgt[3];
 #pragma unroll
     for (int ax = 0; ax < A; ++ax) {
@@ -151,15 +170,29 @@ __device__ __forceinline__ void swarm_step(const ChainConsts<Topo::J>& cc, Swarm
         for (int ax = 0; ax < A; ++ax) {
             const int d = A * (k - 1) + ax;
             if (MASK && !dim_free(cc, d)) continue;  // locked: stays at rest
-            pso_update<MODE>(x[d], v[d], cpb[ax], cg[ax], coef, rng);
+            if constexpr (AHEAD)
+                pso_update_drawn(x[d], v[d], cpb[ax], cg[ax], nd[ax][0], nd[ax][1], nd[ax][2]);
+            else
+                pso_update<MODE>(x[d], v[d], cpb[ax], cg[ax], coef, rng);
             if constexpr (TERMS & kTermUniformBounds)
                 x[d] = clamp_mode<MODE>(x[d], cc.lo[0], cc.hi[0]);
             else
                 x[d] = clamp_mode<MODE>(x[d], sh.lo[d], sh.hi[d]);
         }
+        if constexpr (AHEAD) {
+            if (k < J) {
+#pragma unroll
+                for (int ax = 0; ax < A; ++ax) {
+                    nd[ax][0] = rng.scaled(coef.wq, coef.wh);
+                    nd[ax][1] = rng.scaled(coef.c1q, coef.c1h);
+                    nd[ax][2] = rng.scaled(coef.c2q, coef.c2h);
+                }
+            }
+        }
         acc.node(cc, k, x + A * (k - 1), crest, ctgt, nullptr);
 #if !IKPSO_RES_NO_NODE_BARRIER
-        if (!Topo::kDH || IKPSO_DH_NODE_BARRIER) __builtin_amdgcn_sched_barrier(0);
+        if ((!Topo::kDH || IKPSO_DH_NODE_BARRIER) && (k % IKPSO_NODE_BARRIER_EVERY == 0 || k == J))
+            __builtin_amdgcn_sched_barrier(0);
 #endif
     }
 
@@ -203,10 +236,11 @@ __global__ void __launch_bounds__(kResidentMaxThreads<Topo::D>())
     const int P = io.P;
     const bool active = tid < P;
 
-    __shared__ SwarmShared<Topo> sh;
-    // Local-best positions, [d][lane]: read once per iteration by the update,
-    // written on improvement; consecutive lanes hit consecutive banks.
-    __shared__ float s_pb[D * BLOCK];
+    // Local-best positions lds.pb [d][lane]: read once per iteration by the
+    // update, written on improvement; consecutive lanes hit consecutive banks.
+    __shared__ SwarmLds<Topo, D * BLOCK> lds;
+    SwarmShared<Topo>& sh = lds.sh;
+    float* const s_pb = lds.pb;
     stage_swarm_inputs<Topo>(cc, io.targets, io.start_pose, b, sh);
 
     RngFor<TERMS> rng{0, 0, 0, 0, 0, 0};
@@ -217,7 +251,7 @@ __global__ void __launch_bounds__(kResidentMaxThreads<Topo::D>())
     float x[D], v[D];
     init_particle<Topo, TERMS, BLOCK>(cc, sh, s_pb, tid, x, v, rng);
     // initLocalBests (src/kernel.cu:191-200)
-    float pbf = fitness<Topo, MODE, TERMS>(cc, x, sh.rest, sh.tgt, nullptr, sh.dh);
+    float pbf = fitness<Topo, MODE, TERMS>(cc, x, sh.rest, sh.tgt, nullptr, sh.dh, sh.soft);
 
     // swarm argmin + unconditional first global-best copy (src/kernel.cu:297-304)
     int bidx;
@@ -300,7 +334,7 @@ __global__ void __launch_bounds__(256) k_evaluate(const ChainConsts<Topo::J> cc,
 #pragma unroll
             for (int d = 0; d < 3 * J; ++d) tgt[d] = cc.tgt0[d];
         }
-        const float f = fitness<Topo, MODE, TERMS>(cc, x, rest, tgt, pos);
+        const float f = fitness<Topo, MODE, TERMS>(cc, x, rest, tgt, pos, nullptr, cc.aux + 4 * J);
         if (io.out_fitness) io.out_fitness[n] = f;
         if (io.out_positions) {
 #pragma unroll

@@ -118,7 +118,7 @@ __global__ void __launch_bounds__(kStreamChunk) k_stream_init(const ChainConsts<
                 pl.st(1, d, __builtin_fmaf(rng.uniform(), 2.0f, -1.0f));
             pl.st(2, d, x[d]);
         }
-        pbf = fitness<Topo, MODE, TERMS>(cc, x, sh.rest, sh.tgt, nullptr, sh.dh);
+        pbf = fitness<Topo, MODE, TERMS>(cc, x, sh.rest, sh.tgt, nullptr, sh.dh, sh.soft);
         io.pbf[b * P + i] = pbf;
         const int64_t n = io.num_swarms * P, k = b * P + i;
         io.rng[0 * n + k] = rng.d;
@@ -167,7 +167,7 @@ __global__ void __launch_bounds__(kStreamChunk) k_stream_step(const ChainConsts<
         // update-all-then-evaluate with the same values and accumulation order,
         // while only a handful of angles are live at a time.
         const PsoCoef coef = pso_coef(cc);
-        FitnessFor<Topo, MODE, TERMS> acc(cc, sh.dh);
+        FitnessFor<Topo, MODE, TERMS> acc(cc, sh.dh, sh.soft);
         // Loads are software-pipelined AHEAD nodes ahead (a ring of AHEAD+1
         // node slots in registers, indices resolved at compile time) and every
         // node ends in a scheduling barrier: left alone, the compiler hoists

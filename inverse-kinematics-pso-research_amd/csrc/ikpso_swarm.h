@@ -47,8 +47,23 @@ struct SwarmShared {
     float tgt[3 * J];            // effector targets per node (k-1), 0 elsewhere
     float g[D];                  // global-best vector
     float dh[Topo::kDH ? 12 * J + 4 : 1];  // folded-chain constants (TopoDH)
+    float soft[6 * J];           // soft joint limits [lo 3J | hi 3J] (penalty term): read every
+                                 // iteration, so from LDS rather than the aux array in HBM
     uint32_t key[2][16];         // per-wave argmin, double-buffered by parity
     int32_t idx[2][16];
+};
+
+// A swarm kernel's whole LDS as one object, the uniforms first: LDS addresses
+// below 64 KiB fit a ds_read's 16-bit offset field, so every broadcast read of
+// a uniform (sh.g[d], sh.rest[d], ...) addresses off one zero register.  Two
+// separate __shared__ arrays may be laid out local bests first, putting the
+// uniforms above 64 KiB, where every such read first materialises its absolute
+// address with a v_mov (40 per iteration on the reference scene, 98 at D = 60).
+template <class Topo, int NPB, class Extra = char>
+struct SwarmLds {
+    SwarmShared<Topo> sh;
+    Extra extra;
+    float pb[NPB];  // local bests [d][lane] (the cooperative long-chain build: velocities)
 };
 
 // start_pose: [B][dfree] over the free dimensions (the chain's mask).
@@ -69,6 +84,8 @@ __device__ __forceinline__ void stage_swarm_inputs(const ChainConsts<Topo::J>& c
     }
     if constexpr (Topo::kDH)
         for (int n = threadIdx.x; n < 12 * J + 4; n += blockDim.x) sh.dh[n] = cc.aux[cc.dh_off + n];
+    if (cc.use_penalty)
+        for (int n = threadIdx.x; n < 6 * J; n += blockDim.x) sh.soft[n] = cc.aux[4 * J + n];
 }
 
 // The swarm's answer over the free dimensions: out[b][dfree] from the kernel's

@@ -1,10 +1,14 @@
 #!/bin/bash
-# build_variants.sh NAME "FLAGS" [NAME "FLAGS" ...] -> variants/libikpso_NAME.so
-cd "$(dirname "$0")/../inverse-kinematics-pso-research_amd/csrc"
-pids=()
-while [ $# -ge 2 ]; do
-  name=$1; flags=$2; shift 2
-  make -s -j8 OUT=../../variants/libikpso_$name.so BUILD=_build_$name EXTRA="$flags" >/tmp/bv_$name.log 2>&1 &
-  pids+=($!)
-done
-rc=0; for p in "${pids[@]}"; do wait $p || rc=1; done; exit $rc
+# Experiment builds of libikpso.so for tools/variant_bench.py: one topology
+# subset, one build directory and one output per variant.
+#   tools/build_variants.sh SUBSET NAME [EXTRA FLAGS...]      (current tree)
+#   HEAD_TREE=/path/to/checkout tools/build_variants.sh ...    (another tree)
+# SUBSET: SERIAL20_ONLY | REF7_ONLY.  Output: variants/NAME.so (git-ignored).
+set -e
+ROOT=$(cd "$(dirname "$0")/.." && pwd)
+SUBSET=$1; NAME=$2; shift 2
+SRC=${HEAD_TREE:-$ROOT}/inverse-kinematics-pso-research_amd/csrc
+mkdir -p "$ROOT/variants"
+make -C "$SRC" -j8 BUILD="/tmp/ikpso_var_$NAME" OUT="$ROOT/variants/$NAME.so" \
+     EXTRA="-DIKPSO_EXPERIMENT_$SUBSET $*" > "/tmp/ikpso_var_$NAME.log" 2>&1 || { tail -30 "/tmp/ikpso_var_$NAME.log"; exit 1; }
+echo "built variants/$NAME.so"

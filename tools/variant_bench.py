@@ -34,9 +34,11 @@ def main():
     ap.add_argument("--iters", type=int, default=500)
     ap.add_argument("--arith", default="fast")
     ap.add_argument("--config", type=int, default=3, choices=[3, 5])
+    ap.add_argument("--particles", type=int, default=0, help="override the workload's swarm size")
+    ap.add_argument("--kernel", type=int, default=0, help="ikpso_solver_desc.kernel (0 = AUTO)")
     a = ap.parse_args()
     wl = ikpso.workload(a.config)
-    P, I, B = wl.particles, a.iters, a.swarms
+    P, I, B = a.particles or wl.particles, a.iters, a.swarms
     D = 3 * (wl.chain.shape[0] - 1)
     tg = torch.from_numpy(wl.targets(0, B)).cuda()
     outs = [torch.empty((B, D), device="cuda"), torch.empty(B, device="cuda"), torch.empty(B, device="cuda")]
@@ -51,6 +53,7 @@ def main():
         desc.pso = _abi.PSOConfig(0.5, 0.5, 1.25, I)
         desc.fit = _abi.FitnessConfig(3.0, 0.0, 0.1)
         desc.arith = 0 if a.arith == "fast" else 1
+        desc.kernel = a.kernel
         keep = []
         if wl.limit_weight:
             lo = np.ascontiguousarray(wl.soft_lo, np.float32)
