@@ -225,9 +225,12 @@ __device__ __forceinline__ void init_particle(const ChainConsts<Topo::J>& cc, co
 }
 
 // ------------------------------------------------------- resident swarm kernel
+// The kernel body over its LDS: the per-swarm uniforms `sh` and the local-best
+// positions s_pb[d * BLOCK + lane] (read once per iteration by the update,
+// written on improvement; consecutive lanes hit consecutive banks).
 template <class Topo, int MODE, int TERMS>
-__global__ void __launch_bounds__(kResidentMaxThreads<Topo::D>())
-    k_swarm_resident(const ChainConsts<Topo::J> cc, const SwarmIO io)
+__device__ __forceinline__ void swarm_resident_body(const ChainConsts<Topo::J>& cc, const SwarmIO& io,
+                                                    SwarmShared<Topo>& sh, float* const s_pb)
 {
     constexpr int D = Topo::D;
     constexpr int BLOCK = kResidentMaxThreads<D>();
@@ -236,11 +239,6 @@ __global__ void __launch_bounds__(kResidentMaxThreads<Topo::D>())
     const int P = io.P;
     const bool active = tid < P;
 
-    // Local-best positions lds.pb [d][lane]: read once per iteration by the
-    // update, written on improvement; consecutive lanes hit consecutive banks.
-    __shared__ SwarmLds<Topo, D * BLOCK> lds;
-    SwarmShared<Topo>& sh = lds.sh;
-    float* const s_pb = lds.pb;
     stage_swarm_inputs<Topo>(cc, io.targets, io.start_pose, b, sh);
 
     RngFor<TERMS> rng{0, 0, 0, 0, 0, 0};
@@ -301,6 +299,24 @@ __global__ void __launch_bounds__(kResidentMaxThreads<Topo::D>())
             }
         }
         if (io.dump_bests) io.dump_bests[b * P + tid] = pbf;
+    }
+}
+
+
+template <class Topo, int MODE, int TERMS>
+__global__ void __launch_bounds__(kResidentMaxThreads<Topo::D>())
+    k_swarm_resident(const ChainConsts<Topo::J> cc, const SwarmIO io)
+{
+    constexpr int NPB = Topo::D * kResidentMaxThreads<Topo::D>();
+    if constexpr (Topo::kGeneric) {
+        // generic trees keep two arrays: hipcc 7.2 miscompiles them over one
+        // LDS object (an illegal flat-to-LDS check)
+        __shared__ SwarmShared<Topo> sh;
+        __shared__ float s_pb[NPB];
+        swarm_resident_body<Topo, MODE, TERMS>(cc, io, sh, s_pb);
+    } else {
+        __shared__ SwarmLds<Topo, NPB> lds;  // uniforms below 64 KiB (SwarmLds)
+        swarm_resident_body<Topo, MODE, TERMS>(cc, io, lds.sh, lds.pb);
     }
 }
 

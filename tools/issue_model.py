@@ -20,13 +20,19 @@ COST4 = ("v_lshlrev_b32", "v_add3_u32", "v_cvt_f32_u32", "v_cvt_f32_i32", "v_cvt
 TRANS = ("v_sin_f32", "v_cos_f32", "v_exp_f32", "v_log_f32", "v_rcp_f32", "v_rsq_f32", "v_sqrt_f32")
 
 
+# ordinary ops measured individually by the probe (VGPR operands); others 2.2
+COST2 = {"v_mul_f32": 2.17, "v_fmac_f32": 2.29, "v_fma_f32": 2.23, "v_fmaak_f32": 2.05, "v_fmamk_f32": 2.12,
+         "v_sub_f32": 2.19, "v_xor_b32": 2.45, "v_bitop3_b32": 2.48, "v_lshrrev_b32": 2.16, "v_add_u32": 2.30,
+         "v_and_b32": 2.08, "v_mov_b32": 2.12}
+
+
 def cost(op):
     base = re.sub(r"_e(32|64)$|_dpp$|_sdwa$", "", op)
     if base in TRANS:
         return 8.1, "trans"
     if base in COST4:
         return 4.1, "4-cycle"
-    return 2.2, "2-cycle"
+    return COST2.get(base, 2.2), "2-cycle"
 
 
 def hot_loop(path, key):
@@ -45,6 +51,24 @@ def hot_loop(path, key):
         return sum(1 for l in body[lo:hi + 1] if l.strip().startswith("v_"))
     lo, hi = max(loops, key=lambda t: (valu(*t) if valu(*t) < 0.6 * valu(0, len(body) - 1) else -1))
     return body[lo:hi + 1]
+
+
+def model(path, key):
+    """The hot loop's VALU mix and modelled issue cycles (a dict for profiles/valu_per_update.json)."""
+    loop = hot_loop(path, key)
+    ops = collections.Counter(l.split()[0] for l in loop if l.strip().startswith("v_"))
+    n = collections.Counter()
+    cyc = collections.Counter()
+    for op, k in ops.items():
+        c, cls = cost(op)
+        cyc[cls] += c * k
+        n[cls] += k
+    total_n, total_c = sum(n.values()), sum(cyc.values())
+    return {"loop_valu_instr": total_n, "loop_issue_cycles": round(total_c, 1),
+            "mean_cycles_per_instr": round(total_c / total_n, 4),
+            "by_class": {k: {"instr": n[k], "cycles": round(cyc[k], 1)} for k in ("2-cycle", "4-cycle", "trans")},
+            "costs": "tools/probes/valu_probe.hip (profiles/r02/valu_issue_costs.txt): 2.05-2.48 (measured per op) / "
+                     "4.1 / 8.1 SIMD cycles per wave64 op; hot loop = the kernel's PSO iteration loop in its hipcc -S listing"}
 
 
 def main():

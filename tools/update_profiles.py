@@ -2,7 +2,10 @@
 """Collect gpurun_out/<name>_* (tools/gpu_profile.sh) into profiles/<round>/ and
 record the kernel's per-update counters in profiles/valu_per_update.json
 (keyed by the solver's kernel name; bench.py's roofline reads it).
-usage: update_profiles.py ROUND NAME KERNEL_SUBSTRING KEY UPDATES_PER_DISPATCH"""
+usage: update_profiles.py ROUND NAME KERNEL_SUBSTRING KEY UPDATES_PER_DISPATCH [TU ISA_SYMBOL_SUBSTRING]
+With TU (an ikpso_inst_*.hip unit) the unit is compiled to its ISA listing with the
+library's flags and tools/issue_model.py's issue-cycle model of the kernel's hot
+loop is stored with the counters (bench.py's issue-slot roofline reads it)."""
 import collections
 import csv
 import json
@@ -12,6 +15,7 @@ from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
 rnd, name, pat, key, upd = sys.argv[1], sys.argv[2], sys.argv[3], sys.argv[4], int(sys.argv[5])
+tu, sym = (sys.argv[6], sys.argv[7]) if len(sys.argv) > 7 else (None, None)
 out_dir = ROOT / "profiles" / rnd
 out_dir.mkdir(parents=True, exist_ok=True)
 src = ROOT / "gpurun_out"
@@ -51,6 +55,16 @@ res = {
               "SQ_INSTS_VALU * 64 / updates; bytes = (2*FETCH_SIZE + WRITE_SIZE) KiB*1024 / updates",
     "fetch_bytes": fb, "write_bytes": wb, "updates": upd,
 }
+if tu:
+    import subprocess
+    sys.path.insert(0, str(ROOT / "tools"))
+    import issue_model
+    csrc = ROOT / "inverse-kinematics-pso-research_amd" / "csrc"
+    asm = Path("/tmp") / (Path(tu).stem + ".s")
+    subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fno-slp-vectorize",
+                    f"-I{csrc}", f"-I{ROOT / 'include'}", "--cuda-device-only", "-S", str(csrc / tu), "-o", str(asm)],
+                   check=True, capture_output=True)
+    res["issue_model"] = dict(issue_model.model(str(asm), sym), tu=tu, symbol=sym)
 db_path = ROOT / "profiles" / "valu_per_update.json"
 db = json.loads(db_path.read_text()) if db_path.exists() else {}
 if "valu_lane_instr_per_update" in db:  # old single-kernel format
