@@ -44,8 +44,8 @@
 #endif
 
 // FAST-mode sin/cos on the transcendental unit (v_sin_f32 / v_cos_f32) in the
-// kernels that run 4 waves per SIMD (chains of <= 10 joints) and have no
-// collider term; see sincos_fast.
+// kernels of chains up to 20 joints (D <= 60) that have no collider term; see
+// sincos_fast.
 #ifndef IKPSO_SINCOS_HW
 #define IKPSO_SINCOS_HW 1
 #endif
@@ -190,8 +190,8 @@ __host__ __device__ __forceinline__ void sincos_fast(float x, float* s_out, floa
         // abs error 4.8e-7 on [0, 2pi] and 2.7e-7 on [-pi, pi] (vs 6e-8 for the
         // polynomial); 8 cycles per wave64 op each (tools/probes/valu_probe.hip),
         // 3 instructions per angle against ~20 for the polynomial: -7 % kernel
-        // time on the reference scene.  With 2 waves per SIMD (long chains) the
-        // transcendental latency is exposed and the polynomial is faster (+13 %).
+        // time on the reference scene, -9 % on the 2-wave D = 60 cooperative
+        // kernel once its loop stopped spilling (it was +13 % before).
         const float rev = x * 0.159154943091895336f;
         *s_out = __builtin_amdgcn_sinf(rev);
         *c_out = __builtin_amdgcn_cosf(rev);
