@@ -520,14 +520,20 @@ hipError_t carve_coop(SwarmIO& io, void* ws, int G, int NG, int block, int D, hi
 {
     io.coop_spin_limit = coop_spin_limit();
     Carver cv{static_cast<char*>(ws)};
-    io.coop_counter = cv.take<uint32_t>((size_t)NG * kCoopCounterStride);
     io.coop_error = cv.take<int32_t>(1);
-    io.coop_slots = cv.take<float>((size_t)NG * 2 * G * kCoopSlot(D));
+    io.coop_slots = cv.take<unsigned long long>((size_t)NG * 2 * G * kCoopSlot(D));
     io.coop_pbest = coop_global_pbest(D) ? cv.take<float>((size_t)NG * G * D * block) : nullptr;
+    io.coop_timing = IKPSO_COOP_TIMING ? cv.take<unsigned long long>((size_t)NG * G * 4) : nullptr;
     io.coop_g = G;
     io.coop_ng = NG;
     io.coop_block = block;
-    const size_t zero = reinterpret_cast<char*>(io.coop_slots) - static_cast<char*>(ws);
+    // the error flag and every granule's tag start at 0 (tags are exchange numbers + 1)
+    const size_t zero = reinterpret_cast<char*>(io.coop_slots + (size_t)NG * 2 * G * kCoopSlot(D)) -
+                        static_cast<char*>(ws);
+    if (IKPSO_COOP_TIMING) {
+        const hipError_t e = hipMemsetAsync(io.coop_timing, 0, (size_t)NG * G * 32, s);
+        if (e != hipSuccess) return e;
+    }
     return hipMemsetAsync(ws, 0, zero, s);
 }
 
@@ -583,6 +589,10 @@ struct ikpso_solver {
         const int32_t* error = nullptr;  // device flag in ws
     } pending;
     int64_t fallbacks = 0;
+#if IKPSO_COOP_TIMING
+    unsigned long long* pending_timing = nullptr;
+    int pending_timing_n = 0;
+#endif
 };
 
 namespace {
@@ -976,6 +986,10 @@ ikpso_status ikpso_solve_batch(ikpso_solver* s, const float* targets, const floa
         s->pending.out_residual = out_residual;
         s->pending.stream = hs;
         s->pending.error = io.coop_error;
+#if IKPSO_COOP_TIMING
+        s->pending_timing = io.coop_timing;
+        s->pending_timing_n = NG * G;
+#endif
         return IKPSO_OK;
     }
     return solve_streaming(s, &s->ws, &s->ws_bytes, targets, start_pose, num_swarms, iterations, out_angles,
@@ -991,6 +1005,18 @@ ikpso_status ikpso_solver_sync(ikpso_solver* s)
     int32_t err = 0;
     IKPSO_HIP(hipMemcpyAsync(&err, p.error, sizeof(err), hipMemcpyDeviceToHost, p.stream));
     IKPSO_HIP(hipStreamSynchronize(p.stream));
+#if IKPSO_COOP_TIMING
+    if (s->pending_timing) {  // measurement build: mean cycles per iteration over the workgroups
+        std::vector<unsigned long long> t((size_t)s->pending_timing_n * 4);
+        IKPSO_HIP(hipMemcpy(t.data(), s->pending_timing, t.size() * 8, hipMemcpyDeviceToHost));
+        double a = 0, b = 0, c = 0, it = 0;
+        for (size_t i = 0; i < t.size(); i += 4) a += t[i], b += t[i + 1], it += t[i + 2], c += t[i + 3];
+        fprintf(stderr,
+                "ikpso coop timing: %d workgroups, per iteration (wave 0): step %.0f, argmin barrier %.0f, "
+                "hand-off %.0f cycles\n",
+                s->pending_timing_n, a / it, c / it, b / it);
+    }
+#endif
     if (!err) return IKPSO_OK;
     // A group gave up waiting for its members (the GPU is shared): restore the
     // generator states and solve the whole batch on the streaming kernels.

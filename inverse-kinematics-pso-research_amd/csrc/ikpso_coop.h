@@ -10,23 +10,28 @@
 // per iteration to form the swarm's argmin (thrust::min_element +
 // `globalMin > currentGlobalMin`, src/kernel.cu:297-323):
 //
-//   each chunk: local argmin (first minimum) -> wave 0 publishes {key, index,
-//   winner's local best} to slot [exchange & 1][chunk] with write-through
-//   (sc1) stores -> s_waitcnt vmcnt(0) -> one agent-scope atomic add on the
-//   group's arrival counter -> lane 0 polls the counter (sc1 loads, s_sleep)
-//   until all G chunks of this exchange have arrived -> wave 0 reduces the G
+//   each chunk: local argmin (first minimum) -> wave 0 publishes its record
+//   for exchange e -- the key and the winner's local best, each value in an
+//   8-byte granule {value, tag = e + 1} written by ONE `sc1` store (lane l
+//   writes granule l) -> wave 0 polls the G key granules (lanes 0..G-1,
+//   `global_load_dwordx2 sc1`) until every tag reads e + 1 -> reduces the G
 //   keys in chunk order (ties keep the lowest chunk = lowest particle index)
-//   and, on strict improvement, copies the winner's vector into LDS ->
-//   workgroup barrier.
+//   -> on strict improvement takes the winner's vector (its own from LDS, or
+//   the winner's D granules, re-polled until every tag reads e + 1) into LDS
+//   -> workgroup barrier.
 //
-// This is the hand-off of MI355X_MICROARCH.md's first table row (one storing
-// wave signals after its own vmcnt wait; sc1 stores and loads on both sides;
-// one workgroup per CU; hipMalloc'd memory), so no L2 write-back/invalidate
-// fence is needed.  Slots are double-buffered by exchange parity: a chunk
-// rewrites parity p only after the wait of the previous exchange, by which
-// time every chunk has read parity p.  Workgroup b sits on XCD b % 8; the G
-// chunks of a group share an XCD (speed only, never correctness).  Waits are
-// bounded: a timed-out wait sets io.coop_error and the kernel drains.
+// This is MI355X_MICROARCH.md's tagged-granule hand-off (handoff-1to1: one
+// hop, ~1 us; a separate flag or counter costs 1.7-1.9x that per hop, and the
+// counter protocol this replaces chained four hops: ~12k cycles of a 31k-cycle
+// iteration at D = 60).  A granule is written whole by one store and carries
+// its own exchange number, so no store needs a vmcnt wait and no load needs a
+// fence.  Records are double-buffered by exchange parity: a chunk rewrites
+// parity p only after it has seen every chunk's record of the previous
+// exchange, by which time every chunk has finished reading parity p.  The
+// slots are zeroed before every launch (tag 0 never matches).  Workgroup b sits
+// on XCD b % 8; the G chunks of a group share an XCD (speed only, never
+// correctness).  Waits are bounded: a timed-out wait sets io.coop_error and
+// the kernel drains.
 // Residency is checked at launch against the occupancy query.
 #pragma once
 
@@ -39,17 +44,17 @@
 namespace ikpso {
 
 
-__device__ __forceinline__ void st_sc1(float* p, float v)
+// 8-byte granule access with agent scope: `global_store/load_dwordx2 sc1`
+// (global, never flat: the pointer is cast to the global address space).
+using granule_t = unsigned long long;
+typedef __attribute__((address_space(1))) granule_t global_granule;
+__device__ __forceinline__ void st_granule(granule_t* p, granule_t v)
 {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store((global_granule*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ __forceinline__ float ld_sc1(const float* p)
+__device__ __forceinline__ granule_t ld_granule(const granule_t* p)
 {
-    return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ uint32_t ld_sc1(const uint32_t* p)
-{
-    return __hip_atomic_load(const_cast<uint32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return __hip_atomic_load((global_granule*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Per-workgroup bookkeeping in LDS, read at its points of use: held in SGPRs
@@ -64,8 +69,10 @@ struct CoopShared {
     uint32_t e;         // exchanges of this group so far (identical in every member)
     int32_t pad_;
     int64_t b;          // current swarm
-    uint32_t* counter;  // the group's arrival counter
-    float* slots;       // the group's [2][G] published records
+    granule_t* slots;   // the group's [2][G] published records (kCoopSlot granules each)
+#if IKPSO_COOP_TIMING
+    unsigned long long t_mid;  // wave 0 past the local argmin (timing builds)
+#endif
 };
 
 // Exchange `e` of a group: publish this chunk's local argmin, wait for the G
@@ -112,7 +119,7 @@ __device__ __forceinline__ void coop_exchange(SwarmShared<Topo>& sh, CoopShared<
 {
     constexpr int D = Topo::D;
     constexpr int SLOT = kCoopSlot(D);
-    static_assert(D + 2 <= 64, "wave 0 publishes the record in one store instruction");
+    static_assert(D + 1 <= 64, "wave 0 publishes the record in one store instruction");
     int lidx;
     const uint32_t lmin = swarm_argmin(sh, 0, local_key, &lidx);  // one workgroup barrier inside
 #if IKPSO_COOP_NO_EXCHANGE  // timing-only ablation: every chunk its own swarm (no cross-CU hand-off)
@@ -129,43 +136,49 @@ __device__ __forceinline__ void coop_exchange(SwarmShared<Topo>& sh, CoopShared<
 #endif
     if (wave_id() == 0) {
         compiler_fence();
+#if IKPSO_COOP_TIMING
+        cs.t_mid = __builtin_amdgcn_s_memtime();
+#endif
         const int G = cs.G, member = cs.member;
         const uint32_t e = cs.e;
-        uint32_t* counter = cs.counter;
-        float* slots = cs.slots;
         const int lane = lane_id_here();
-        float* base = slots + (size_t)(e & 1) * G * SLOT;
-        float* mine = base + (size_t)member * SLOT;
-        // lanes 0..D-1: the winner's local best; lane D: key; lane D+1: global index
-        if (lane < D) st_sc1(mine + 2 + lane, local_best<BLOCK>(s_pb, lane, lidx));
-        if (lane == D) st_sc1(mine, __uint_as_float(lmin));
-        if (lane == D + 1) st_sc1(mine + 1, __int_as_float(member * BLOCK + lidx));
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const uint32_t target = (uint32_t)G * (e + 1);
+        const granule_t tag = (granule_t)(e + 1) << 32;
+        granule_t* base = cs.slots + (size_t)(e & 1) * G * SLOT;
+        // granule 0: the key; granules 1..D: the chunk winner's local best
+        const float mine_d = lane >= 1 && lane <= D ? local_best<BLOCK>(s_pb, lane - 1, lidx) : 0.0f;
+        if (lane <= D) st_granule(base + (size_t)member * SLOT + lane, tag | (lane == 0 ? lmin : __float_as_uint(mine_d)));
+        // the G key granules, in chunk order (lanes 0..G-1; G <= 64)
+        uint32_t n = 0;
         int timed_out = 0;
-        if (lane == 0) {
-            __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            uint32_t n = 0;
-            if (spin_limit == 0)  // debug knob (IKPSO_COOP_SPIN_LIMIT=0): always take the give-up path
+        granule_t kg;
+        for (;;) {
+            kg = lane < G ? ld_granule(base + (size_t)lane * SLOT) : tag;
+            if (__builtin_amdgcn_ballot_w64((kg >> 32) != (granule_t)(e + 1)) == 0) break;
+            if (spin_limit == 0 || n++ >= spin_limit) {  // spin_limit 0 (IKPSO_COOP_SPIN_LIMIT=0): the give-up path
                 timed_out = 1;
-            else
-                while (ld_sc1(counter) < target) {
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        const uint32_t k = lane < G ? (uint32_t)kg : 0xFFFFFFFFu;
+        const uint32_t gmin = wave_min_u32(k);
+        const int wj = wave_first_lane_eq(k, gmin);
+        const uint32_t cur = cs.gkey;
+        if (!timed_out && (force || gmin < cur)) {  // uniform within wave 0
+            float gv = mine_d;  // this chunk won: its own vector, no hop
+            if (wj != member) {
+                granule_t vg;
+                for (;;) {  // the winner's D granules (their tags already read e + 1 in practice)
+                    vg = lane >= 1 && lane <= D ? ld_granule(base + (size_t)wj * SLOT + lane) : tag;
+                    if (__builtin_amdgcn_ballot_w64((vg >> 32) != (granule_t)(e + 1)) == 0) break;
                     if (n++ >= spin_limit) {
                         timed_out = 1;
                         break;
                     }
-                    __builtin_amdgcn_s_sleep(2);
                 }
-        }
-        timed_out = __builtin_amdgcn_readfirstlane(timed_out);  // lane 0's verdict
-        asm volatile("" ::: "memory");
-        // the G chunk keys, in chunk order (lanes 0..G-1; G <= 64)
-        const uint32_t k = lane < G ? __float_as_uint(ld_sc1(base + (size_t)lane * SLOT)) : 0xFFFFFFFFu;
-        const uint32_t gmin = wave_min_u32(k);
-        const int wj = wave_first_lane_eq(k, gmin);
-        const uint32_t cur = cs.gkey;
-        if (force || gmin < cur) {  // uniform within wave 0
-            if (lane < D) sh.g[lane] = ld_sc1(base + (size_t)wj * SLOT + 2 + lane);
+                gv = __uint_as_float((uint32_t)vg);
+            }
+            if (lane >= 1 && lane <= D) sh.g[lane - 1] = gv;
             if (lane == 0) cs.gkey = gmin;
         }
         if (lane == 0) {
@@ -297,7 +310,6 @@ __global__ void __launch_bounds__(BLOCK, (BLOCK >= 256 ? BLOCK / 256 : 1))
         cs.e = 0;
         cs.abort = 0;
         cs.b = group;
-        cs.counter = io.coop_counter + (size_t)group * kCoopCounterStride;
         cs.slots = io.coop_slots + (size_t)group * 2 * G * kCoopSlot(D);
     }
     __syncthreads();
@@ -339,20 +351,45 @@ __global__ void __launch_bounds__(BLOCK, (BLOCK >= 256 ? BLOCK / 256 : 1))
         else
             coop_exchange<Topo, BLOCK>(sh, cs, s_pb, key0, io.coop_error, io.coop_spin_limit, true);
 
+#if IKPSO_COOP_TIMING
+        unsigned long long t_step = 0, t_bar = 0, t_exch = 0, n_it = 0;
+#endif
         for (int it = 0; it < io.iterations; ++it) {
             compiler_fence();
             if (cs.abort) break;
+#if IKPSO_COOP_TIMING
+            const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+#endif
             if constexpr (PBG)
                 swarm_step_pbg<Topo, MODE, TERMS, BLOCK>(cc, sh, s_pb, pbg, tid, x, pbf, coef, rng);
             else
                 swarm_step<Topo, MODE, TERMS, BLOCK>(cc, sh, s_pb, tid, x, v, pbf, coef, rng);
             const bool act = cs.member * BLOCK + tid < P;
             const uint32_t key = act ? ordered_key(pbf) : 0xFFFFFFFFu;
+#if IKPSO_COOP_TIMING
+            const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+#endif
             if constexpr (PBG)
                 coop_exchange<Topo, BLOCK>(sh, cs, pbg, key, io.coop_error, io.coop_spin_limit, false);
             else
                 coop_exchange<Topo, BLOCK>(sh, cs, s_pb, key, io.coop_error, io.coop_spin_limit, false);
+#if IKPSO_COOP_TIMING
+            const unsigned long long t2 = __builtin_amdgcn_s_memtime();
+            t_step += t1 - t0;  // wave 0's own step
+            t_bar += cs.t_mid - t1;  // the local argmin: waiting at its barrier for the other waves' steps
+            t_exch += t2 - cs.t_mid;  // the cross-CU hand-off + the closing barrier
+            ++n_it;
+#endif
         }
+#if IKPSO_COOP_TIMING
+        if (tid == 0) {
+            unsigned long long* tm = io.coop_timing + (size_t)blockIdx.x * 4;
+            tm[0] += t_step;
+            tm[1] += t_exch;
+            tm[2] += n_it;
+            tm[3] += t_bar;
+        }
+#endif
 
         compiler_fence();
         const int member = cs.member;

@@ -98,16 +98,17 @@ __host__ __device__ constexpr int kCoopThreads()
 // loop and 3958 issue slots per update instead of 4651, yet 119-122 ms against
 // 97.6 ms -- the LDS velocity round trip and the global loads cost more than the
 // registers they free at 2 waves per SIMD.
+#ifndef IKPSO_COOP_TIMING
+#define IKPSO_COOP_TIMING 0  // measurement builds: per-workgroup cycles in the step and in the hand-off
+#endif
 #ifndef IKPSO_COOP_PBG
 #define IKPSO_COOP_PBG 0
 #endif
 __host__ __device__ constexpr bool coop_global_pbest(int D) { return IKPSO_COOP_PBG && D > 30; }
 
-// Published record of one chunk: key, global particle index, D floats, padded
-// to a 64-B multiple.
-__host__ __device__ constexpr int kCoopSlot(int D) { return ((D + 2 + 15) / 16) * 16; }
-
-constexpr int kCoopCounterStride = 32;
+// Published record of one chunk, in 8-byte granules {value, tag}: the key, then
+// the D floats of the chunk winner's local best; padded to a 128-B multiple.
+__host__ __device__ constexpr int kCoopSlot(int D) { return ((D + 1 + 15) / 16) * 16; }
 // Default bound on a cooperative group wait (polls of ~1 us each): seconds,
 // against ~2 us per exchange when the group is co-resident.
 // IKPSO_COOP_SPIN_LIMIT overrides it (0 forces the give-up path: fallback tests).

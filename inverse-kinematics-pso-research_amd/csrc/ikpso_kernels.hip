@@ -116,8 +116,8 @@ hipError_t launch_evaluate(const ChainHost& ch, int mode, const EvalIO& io, hipS
 hipError_t launch_coop(const ChainHost& ch, int mode, const SwarmIO& io, hipStream_t stream)
 {
     if (io.num_swarms <= 0) return hipSuccess;
-    if (!ch.aux_dev || io.coop_g <= 0 || io.coop_ng <= 0 || io.coop_ng % 8 != 0 || !io.coop_counter ||
-        !io.coop_slots || !io.coop_error)
+    if (!ch.aux_dev || io.coop_g <= 0 || io.coop_ng <= 0 || io.coop_ng % 8 != 0 || !io.coop_slots ||
+        !io.coop_error)
         return hipErrorInvalidValue;
     hipError_t err = hipErrorInvalidValue;
     const bool ok = visit_topology(ch, [&](auto topo) {
@@ -154,8 +154,8 @@ bool coop_geometry(const ChainHost& ch, int mode, CoopGeometry* g)
 size_t coop_workspace_bytes(int ng, int G, int D, int block)
 {
     const size_t pbg = coop_global_pbest(D) ? sizeof(float) * (size_t)ng * G * D * block + 256 : 0;
-    return sizeof(uint32_t) * (size_t)ng * kCoopCounterStride + sizeof(float) * (size_t)ng * 2 * G * kCoopSlot(D) +
-           256 + 3 * 256 + pbg;
+    return 8 * (size_t)ng * 2 * G * kCoopSlot(D) +
+           256 + 3 * 256 + pbg + (IKPSO_COOP_TIMING ? 32 * (size_t)ng * G + 256 : 0);
 }
 
 hipError_t launch_stream(const ChainHost& ch, int mode, const StreamIO& io, int iterations, hipStream_t stream)

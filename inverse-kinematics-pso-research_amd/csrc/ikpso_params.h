@@ -65,14 +65,15 @@ struct SwarmIO {
     int32_t iterations;
     int64_t num_swarms;
     // cooperative kernel only (ikpso_coop.h): G workgroups per swarm, NG groups
-    uint32_t* coop_counter;   // [NG][32] arrival counters (zeroed before the launch)
-    float* coop_slots;        // [NG][2][G][kCoopSlot(D)] published chunk minima
+    unsigned long long* coop_slots;  // [NG][2][G][kCoopSlot(D)] granules {value, tag}: the chunk minima (zeroed
+                                     // before the launch)
     int32_t* coop_error;      // set to 1 if a group wait timed out
     int32_t coop_g;
     int32_t coop_ng;
     int32_t coop_block;       // workgroup size (kCoopThreads<J>() or kCoopLatencyThreads)
     uint32_t coop_spin_limit; // polls before a group wait gives up (0: give up at the first unmet poll)
     float* coop_pbest;        // [NG*G][D][BLOCK] local-best planes of the long-chain build (coop_global_pbest)
+    unsigned long long* coop_timing;  // IKPSO_COOP_TIMING builds: [NG*G][4] cycle counts (else null)
 };
 
 // Streaming (state-in-HBM) kernels: one launch per PSO iteration over every

@@ -75,6 +75,7 @@ def main():
             assert lib.ikpso_solve_batch(h, tg.data_ptr(), None, B, I, outs[0].data_ptr(), outs[1].data_ptr(),
                                          outs[2].data_ptr(), None) == 0
             e1.record()
+            assert lib.ikpso_solver_sync(h) == 0  # settles a cooperative solve (the timing build reports here)
             torch.cuda.synchronize()
             if r:
                 times[p].append(e0.elapsed_time(e1))
