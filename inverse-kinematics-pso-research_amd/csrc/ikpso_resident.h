@@ -34,8 +34,38 @@
 #ifndef IKPSO_TRIG_AHEAD_MAX_D
 #define IKPSO_TRIG_AHEAD_MAX_D 30
 #endif
+#ifndef IKPSO_PRIO_LEVEL
+// progress-levelled wave priority inside the iteration: 1 = the long-chain
+// (2-wave) step only, 2 = the pipelined 4-wave step too.  Measured on
+// 2048 swarms x 100 iterations (profiles/r02c/variant_timings): config 5
+// 81.1 -> 77.4 ms; config 3 48.5 -> 51.8 ms (so not there)
+#define IKPSO_PRIO_LEVEL 1
+#endif
+#ifndef IKPSO_PRIO_LEVELS
+#define IKPSO_PRIO_LEVELS 4
+#endif
 
 namespace ikpso {
+
+// Progress-levelled wave priority: entering node k of J a wave sets its issue
+// priority to 3 - 4(k-1)/J, so a wave that has run ahead of the others on its
+// SIMD yields issue slots to the ones behind it.  The waves of a workgroup meet
+// at the swarm argmin's barrier every iteration; under the arbiter's
+// oldest-first tie-break the oldest wave finishes its step first and the last
+// one runs its tail alone, with nothing to hide its dependency latency.
+template <int J, int LEVEL = 1>
+__device__ __forceinline__ void progress_prio(int k)
+{
+    if constexpr (IKPSO_PRIO_LEVEL >= LEVEL) {
+        constexpr int L = IKPSO_PRIO_LEVELS;  // priority levels used, 2..4
+        switch ((L - 1) - (L * (k - 1)) / J) {
+        case 3: __builtin_amdgcn_s_setprio(3); break;
+        case 2: __builtin_amdgcn_s_setprio(2); break;
+        case 1: __builtin_amdgcn_s_setprio(1); break;
+        default: __builtin_amdgcn_s_setprio(0); break;
+        }
+    }
+}
 
 // One PSO iteration of one particle (lane `tid`) of a swarm whose local bests
 // sit in LDS as s_pb[d * BLOCK + lane] (shared by the resident and cooperative
@@ -79,10 +109,12 @@ __device__ __forceinline__ float swarm_step_ahead(const ChainConsts<Topo::J>& cc
     constexpr int J = Topo::J, A = Topo::A;
     constexpr bool HW = kHwTrig<Topo, MODE, TERMS>;
     FitnessFor<Topo, MODE, TERMS> acc(cc, sh.dh, sh.soft);
+    progress_prio<J, 2>(1);
     update_node<Topo, MODE, TERMS, BLOCK>(cc, sh, s_pb, tid, 1, x, v, coef, rng);
     NodeTrig<A> cur = node_trig<HW, A>(x);
 #pragma unroll
     for (int k = 1; k <= J; ++k) {
+        if (k > 1) progress_prio<J, 2>(k);
         NodeTrig<A> nxt = cur;
         if (k < J) {
             update_node<Topo, MODE, TERMS, BLOCK>(cc, sh, s_pb, tid, k + 1, x, v, coef, rng);
@@ -146,6 +178,7 @@ __device__ __forceinline__ void swarm_step(const ChainConsts<Topo::J>& cc, Swarm
     for (int c = 0; c < 3; ++c) ntgt[c] = Topo::effector(1) ? sh.tgt[c] : 0.0f;
 #pragma unroll
     for (int k = 1; k <= J; ++k) {
+        progress_prio<J, (D > IKPSO_TRIG_AHEAD_MAX_D ? 1 : 2)>(k);  // the 2-wave kernels
         float cpb[A], cg[A], crest[A], ctgt[3];
 #pragma unroll
         for (int ax = 0; ax < A; ++ax) {
