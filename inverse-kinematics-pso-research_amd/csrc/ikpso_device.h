@@ -808,6 +808,153 @@ template <class Topo, int MODE, int TERMS>
 using FitnessFor =
     std::conditional_t<Topo::kDH, FitnessAccDH<Topo, MODE, TERMS>, FitnessAcc<Topo, MODE, TERMS>>;
 
+// FAST serial chains whose only position term is the tip (TopoSerialTip; no
+// distance term, colliders or mask, terms known at compile time): the tip is
+// evaluated from the tip back, in the chain's Horner form
+//   p_J = p_0 + R_0 (R_1 (l_1 e_x + R_2 (l_2 e_x + ... R_J (l_J e_x))))
+// with R_k = Rx(a) Ry(b) Rz(c): per node three plane rotations of ONE vector
+// (12 multiply-adds + 1 add) instead of composing the node's world frame (36
+// multiply-adds for the three column rotations + 3 for the position) -- only
+// the tip's position is consumed, so no node's frame is needed.  The angle and
+// penalty terms accumulate in node order exactly as FitnessAcc::terms does.
+template <class Topo>
+struct IsSerialTip : std::false_type {};
+template <int J>
+struct IsSerialTip<TopoSerialTip<J>> : std::true_type {};
+#ifndef IKPSO_TIP_BACKWARD
+#define IKPSO_TIP_BACKWARD 1
+#endif
+template <class Topo, int MODE, int TERMS>
+constexpr bool kTipBackward = IKPSO_TIP_BACKWARD && MODE == IKPSO_ARITH_FAST &&
+                              (IsSerialTip<Topo>::value || Topo::kDH) &&
+                              !(TERMS & (kTermPosRef | kTermRuntime | kTermColliders | kTermMask));
+
+template <class Topo, int MODE, int TERMS>
+struct TipBackAcc {
+    static constexpr int J = Topo::J;
+    static constexpr bool HW = kHwTrig<Topo, MODE, TERMS>;
+    const float* soft;
+    float rot_diff, pen, ux, uy, uz;
+
+    __device__ __forceinline__ TipBackAcc(const float*, const float* soft_) : soft(soft_), rot_diff(0.0f), pen(0.0f) {}
+
+    // node k's angle terms (node order, as FitnessAcc::terms)
+    __device__ __forceinline__ void angles(int k, const float* ang, const float* rest3)
+    {
+        const float dx = rest3[0] - ang[0], dy = rest3[1] - ang[1], dz = rest3[2] - ang[2];
+        rot_diff = rot_diff + ((dx * dx + dy * dy) + dz * dz);
+        if constexpr (TERMS & kTermPenalty) {
+#pragma unroll
+            for (int ax = 0; ax < 3; ++ax) {
+                const int d = 3 * (k - 1) + ax;
+                const float slo = soft[d], shi = soft[3 * J + d];
+                const float over = fmaxf(fmaxf(ang[ax] - shi, slo - ang[ax]), 0.0f);
+                pen = pen + over * over;
+            }
+        }
+    }
+
+    // u <- R_k (l_k e_x + u); nodes from J down to 1 (node J starts from u = 0)
+    __device__ __forceinline__ void back(const ChainConsts<J>& cc, int k, const NodeTrig<3>& t)
+    {
+        const float sa = t.s[0], ca = t.c[0], sb = t.s[1], cb = t.c[1], sc = t.s[2], cc_ = t.c[2];
+        const float l = cc.len[k];
+        float w0, w1, w2;
+        if (k == J) {  // Rz (l, 0, 0)
+            w0 = cc_ * l;
+            w1 = sc * l;
+            w2 = 0.0f;
+        } else {
+            const float a0 = ux + l;
+            w0 = cc_ * a0 - sc * uy;
+            w1 = sc * a0 + cc_ * uy;
+            w2 = uz;
+        }
+        // Ry: (cb w0 + sb w2, w1, cb w2 - sb w0)
+        const float y0 = k == J ? cb * w0 : cb * w0 + sb * w2;
+        const float y2 = k == J ? -(sb * w0) : cb * w2 - sb * w0;
+        // Rx: (y0, ca w1 - sa y2, sa w1 + ca y2)
+        ux = y0;
+        uy = ca * w1 - sa * y2;
+        uz = sa * w1 + ca * y2;
+    }
+
+    // fitness once back() has run for node 1: the tip term + the angle terms
+    __device__ __forceinline__ float finish(const ChainConsts<J>& cc, const float* tgt3) const
+    {
+        const float* m = cc.m0;  // origin frame, row-major 3x4
+        const float px = m[3] + (m[0] * ux + m[1] * uy + m[2] * uz);
+        const float py = m[7] + (m[4] * ux + m[5] * uy + m[6] * uz);
+        const float pz = m[11] + (m[8] * ux + m[9] * uy + m[10] * uz);
+        const float ex = px - tgt3[0], ey = py - tgt3[1], ez = pz - tgt3[2];
+        const float distance = ((ex * ex + ey * ey) + ez * ez) * cc.eff_w[J];
+        float f = distance + cc.aw_j * rot_diff;
+        if constexpr (TERMS & kTermPenalty) f = f + cc.lim_w * pen;
+        return f;
+    }
+};
+
+// The folded chain (TopoDH) from the tip back: tip = q_0 + C_1 Rz(t_1) (s_1 +
+// C_2 Rz(t_2) (s_2 + ... + C_J Rz(t_J) s_J)) -- per joint 3 adds, one plane
+// rotation (4) and C_j times a vector (9) instead of W_{j-1} C_j (27), the
+// column rotation (12) and the position (9) of FitnessAccDH.
+template <class Topo, int MODE, int TERMS>
+struct TipBackAccDH {
+    static constexpr int J = Topo::J;
+    static constexpr bool HW = kHwTrig<Topo, MODE, TERMS>;
+    const float* dhc;
+    const float* soft;
+    float rot_diff, pen, ux, uy, uz;
+
+    __device__ __forceinline__ TipBackAccDH(const float* dh, const float* soft_)
+        : dhc(dh), soft(soft_), rot_diff(0.0f), pen(0.0f)
+    {
+    }
+
+    __device__ __forceinline__ void angles(int k, const float* ang, const float* rest)
+    {
+        const float dt = rest[0] - ang[0];
+        rot_diff = rot_diff + dt * dt;
+        if constexpr (TERMS & kTermPenalty) {
+            const int d = k - 1;
+            const float slo = soft[d], shi = soft[3 * J + d];
+            const float over = fmaxf(fmaxf(ang[0] - shi, slo - ang[0]), 0.0f);
+            pen = pen + over * over;
+        }
+    }
+
+    // u <- C_k Rz(t_k) (s_k + u); joints from J down to 1 (joint J: u = 0)
+    __device__ __forceinline__ void back(const ChainConsts<J>&, int k, const NodeTrig<1>& t)
+    {
+        const float* C = dhc + 12 * (k - 1);
+        const float st = t.s[0], ct = t.c[0];
+        float w0 = C[9], w1 = C[10], w2 = C[11];
+        if (k < J) {
+            w0 = w0 + ux;
+            w1 = w1 + uy;
+            w2 = w2 + uz;
+        }
+        const float r0 = ct * w0 - st * w1, r1 = st * w0 + ct * w1;
+        ux = C[0] * r0 + C[1] * r1 + C[2] * w2;
+        uy = C[3] * r0 + C[4] * r1 + C[5] * w2;
+        uz = C[6] * r0 + C[7] * r1 + C[8] * w2;
+    }
+
+    __device__ __forceinline__ float finish(const ChainConsts<J>& cc, const float* tgt3) const
+    {
+        const float px = dhc[12 * J + 0] + ux, py = dhc[12 * J + 1] + uy, pz = dhc[12 * J + 2] + uz;
+        const float ex = px - tgt3[0], ey = py - tgt3[1], ez = pz - tgt3[2];
+        const float distance = ((ex * ex + ey * ey) + ez * ez) * cc.eff_w[J];
+        float f = distance + cc.aw_j * rot_diff;
+        if constexpr (TERMS & kTermPenalty) f = f + cc.lim_w * pen;
+        return f;
+    }
+};
+
+template <class Topo, int MODE, int TERMS>
+using TipAccFor =
+    std::conditional_t<Topo::kDH, TipBackAccDH<Topo, MODE, TERMS>, TipBackAcc<Topo, MODE, TERMS>>;
+
 // x, rest: [D]; tgt: [3J] (per node); dhc: the folded chain's constants (TopoDH);
 // soft: the soft limits [lo 3J | hi 3J] (SwarmShared::soft, or cc.aux + 4J).
 template <class Topo, int MODE, int TERMS>
@@ -816,6 +963,18 @@ __device__ __forceinline__ float fitness(const ChainConsts<Topo::J>& cc, const f
                                          const float* dhc, const float* soft)
 {
     constexpr int A = Topo::A;
+    if constexpr (kTipBackward<Topo, MODE, TERMS>) {
+        if (!node_pos) {
+            constexpr int J = Topo::J;
+            using Acc = TipAccFor<Topo, MODE, TERMS>;
+            Acc tb(dhc, soft);
+#pragma unroll
+            for (int k = 1; k <= J; ++k) tb.angles(k, x + A * (k - 1), rest + A * (k - 1));
+#pragma unroll
+            for (int k = J; k >= 1; --k) tb.back(cc, k, node_trig<Acc::HW, A>(x + A * (k - 1)));
+            return tb.finish(cc, tgt + 3 * (J - 1));
+        }
+    }
     FitnessFor<Topo, MODE, TERMS> acc(cc, dhc, soft);
 #pragma unroll
     for (int k = 1; k <= Topo::J; ++k) {

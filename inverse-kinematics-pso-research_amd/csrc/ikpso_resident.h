@@ -41,6 +41,9 @@
 // 81.1 -> 77.4 ms; config 3 48.5 -> 51.8 ms (so not there)
 #define IKPSO_PRIO_LEVEL 1
 #endif
+#ifndef IKPSO_TIP_BACKWARD_SHORT
+#define IKPSO_TIP_BACKWARD_SHORT 1  // the tip-backward step in the 4-wave (D <= 30) kernels too
+#endif
 #ifndef IKPSO_PRIO_LEVELS
 #define IKPSO_PRIO_LEVELS 4
 #endif
@@ -134,6 +137,81 @@ __device__ __forceinline__ float swarm_step_ahead(const ChainConsts<Topo::J>& cc
     return acc.finish(cc);
 }
 
+// Serial chains with a tip effector and the folded chain (kTipBackward
+// builds): all J nodes are updated in dimension order (the same draws; the
+// angle terms in node order), then the tip is evaluated from the tip back
+// (TipAccFor), each node's sines and cosines computed one node ahead of its
+// rotation.
+template <class Topo, int MODE, int TERMS, int BLOCK, class Rng>
+__device__ __forceinline__ void swarm_step_tip(const ChainConsts<Topo::J>& cc, SwarmShared<Topo>& sh, float* s_pb,
+                                               int tid, float (&x)[Topo::D], float (&v)[Topo::D], float& pbf,
+                                               const PsoCoef& coef, Rng& rng)
+{
+    constexpr int J = Topo::J, A = Topo::A, D = Topo::D;
+    constexpr int PL = D > IKPSO_TRIG_AHEAD_MAX_D ? 1 : 2;  // wave priority: the 2-wave kernels
+    using Acc = TipAccFor<Topo, MODE, TERMS>;
+    Acc acc(sh.dh, sh.soft);
+    float npb[A], ng[A], nrest[A];
+#pragma unroll
+    for (int ax = 0; ax < A; ++ax) {
+        npb[ax] = s_pb[ax * BLOCK + tid];
+        ng[ax] = sh.g[ax];
+        nrest[ax] = sh.rest[ax];
+    }
+#pragma unroll
+    for (int k = 1; k <= J; ++k) {
+        progress_prio<2 * J, PL>(k);
+        float cpb[A], cg[A], crest[A];
+#pragma unroll
+        for (int ax = 0; ax < A; ++ax) {
+            cpb[ax] = npb[ax];
+            cg[ax] = ng[ax];
+            crest[ax] = nrest[ax];
+        }
+        if (k < J) {
+#pragma unroll
+            for (int ax = 0; ax < A; ++ax) {
+                const int d = A * k + ax;
+                npb[ax] = s_pb[d * BLOCK + tid];
+                ng[ax] = sh.g[d];
+                nrest[ax] = sh.rest[d];
+            }
+        }
+#pragma unroll
+        for (int ax = 0; ax < A; ++ax) {
+            const int d = A * (k - 1) + ax;
+            pso_update<MODE>(x[d], v[d], cpb[ax], cg[ax], coef, rng);
+            if constexpr (TERMS & kTermUniformBounds)
+                x[d] = clamp_mode<MODE>(x[d], cc.lo[0], cc.hi[0]);
+            else
+                x[d] = clamp_mode<MODE>(x[d], sh.lo[d], sh.hi[d]);
+        }
+        acc.angles(k, x + A * (k - 1), crest);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    NodeTrig<A> cur = node_trig<Acc::HW, A>(x + A * (J - 1));
+#pragma unroll
+    for (int k = J; k >= 1; --k) {
+        progress_prio<2 * J, PL>(2 * J + 1 - k);
+        NodeTrig<A> nxt = cur;
+        if (k > 1) nxt = node_trig<Acc::HW, A>(x + A * (k - 2));
+        acc.back(cc, k, cur);
+        cur = nxt;
+        // (the folded chain's constants are LDS reads: left free to be issued ahead)
+        if (!Topo::kDH) __builtin_amdgcn_sched_barrier(0);
+    }
+    float tgt[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) tgt[c] = sh.tgt[3 * (J - 1) + c];
+    // updateLocalBests (src/kernel.cu:202-221): strict improvement
+    const float f = acc.finish(cc, tgt);
+    if (f < pbf) {
+        pbf = f;
+#pragma unroll
+        for (int d = 0; d < D; ++d) s_pb[d * BLOCK + tid] = x[d];
+    }
+}
+
 // Masked chains (kMasked builds): a locked dimension takes no draws and keeps
 // its rest value, as in the oracle's masked restatement.
 template <class Topo, int MODE, int TERMS, int BLOCK, class Rng>
@@ -143,6 +221,10 @@ __device__ __forceinline__ void swarm_step(const ChainConsts<Topo::J>& cc, Swarm
 {
     constexpr int J = Topo::J, A = Topo::A, D = Topo::D;
     constexpr bool MASK = kMasked<Topo, TERMS>;
+    if constexpr (kTipBackward<Topo, MODE, TERMS> && (Topo::D > IKPSO_TRIG_AHEAD_MAX_D || IKPSO_TIP_BACKWARD_SHORT)) {
+        swarm_step_tip<Topo, MODE, TERMS, BLOCK>(cc, sh, s_pb, tid, x, v, pbf, coef, rng);
+        return;
+    }
     if constexpr (MODE == IKPSO_ARITH_FAST && Topo::D <= IKPSO_TRIG_AHEAD_MAX_D) {
         // updateLocalBests (src/kernel.cu:202-221): strict improvement
         const float f = swarm_step_ahead<Topo, MODE, TERMS, BLOCK>(cc, sh, s_pb, tid, x, v, coef, rng);
