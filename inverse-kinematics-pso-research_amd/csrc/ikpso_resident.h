@@ -35,32 +35,39 @@
 #define IKPSO_TRIG_AHEAD_MAX_D 30
 #endif
 #ifndef IKPSO_PRIO_LEVEL
-// progress-levelled wave priority inside the iteration: 1 = the long-chain
-// (2-wave) step only, 2 = the pipelined 4-wave step too.  Measured on
-// 2048 swarms x 100 iterations (profiles/r02c/variant_timings): config 5
-// 81.1 -> 77.4 ms; config 3 48.5 -> 51.8 ms (so not there)
+// progress-levelled wave priority inside the iteration: 0 = off, 1 = the
+// long-chain (2-wave) step over 4 levels and the pipelined 4-wave step over 2,
+// 2 = the 4-wave tip-backward step too.  Measured: config 5 81.1 -> 77.4 ms on
+// 2048 swarms x 100 iterations (profiles/r02c, r02d variant_timings); config 3
+// 48.3 -> 47.3 ms with 2 levels, 51.7 ms with 4 (profiles/r02g); the folded DH
+// arm's 4-wave tip-backward step unchanged within noise (so left off)
 #define IKPSO_PRIO_LEVEL 1
 #endif
 #ifndef IKPSO_TIP_BACKWARD_SHORT
 #define IKPSO_TIP_BACKWARD_SHORT 1  // the tip-backward step in the 4-wave (D <= 30) kernels too
 #endif
 #ifndef IKPSO_PRIO_LEVELS
-#define IKPSO_PRIO_LEVELS 4
+#define IKPSO_PRIO_LEVELS 4  // levels of the 2-wave steps
+#endif
+#ifndef IKPSO_PRIO_LEVELS_4WAVE
+#define IKPSO_PRIO_LEVELS_4WAVE 2  // levels of the pipelined 4-wave step
 #endif
 
 namespace ikpso {
 
 // Progress-levelled wave priority: entering node k of J a wave sets its issue
-// priority to 3 - 4(k-1)/J, so a wave that has run ahead of the others on its
-// SIMD yields issue slots to the ones behind it.  The waves of a workgroup meet
+// priority to (L-1) - L(k-1)/J, so a wave that has run ahead of the others on
+// its SIMD yields issue slots to the ones behind it.  The waves of a workgroup meet
 // at the swarm argmin's barrier every iteration; under the arbiter's
 // oldest-first tie-break the oldest wave finishes its step first and the last
 // one runs its tail alone, with nothing to hide its dependency latency.
-template <int J, int LEVEL = 1>
+// With 4 waves per SIMD, 2 levels (4 keep them in lockstep, contending for the
+// same unit at the same time).
+template <int J, int LEVEL = 1, int L = IKPSO_PRIO_LEVELS>
 __device__ __forceinline__ void progress_prio(int k)
 {
+    static_assert(L >= 2 && L <= 4, "priority levels 2..4");
     if constexpr (IKPSO_PRIO_LEVEL >= LEVEL) {
-        constexpr int L = IKPSO_PRIO_LEVELS;  // priority levels used, 2..4
         switch ((L - 1) - (L * (k - 1)) / J) {
         case 3: __builtin_amdgcn_s_setprio(3); break;
         case 2: __builtin_amdgcn_s_setprio(2); break;
@@ -112,12 +119,12 @@ __device__ __forceinline__ float swarm_step_ahead(const ChainConsts<Topo::J>& cc
     constexpr int J = Topo::J, A = Topo::A;
     constexpr bool HW = kHwTrig<Topo, MODE, TERMS>;
     FitnessFor<Topo, MODE, TERMS> acc(cc, sh.dh, sh.soft);
-    progress_prio<J, 2>(1);
+    progress_prio<J, 1, IKPSO_PRIO_LEVELS_4WAVE>(1);
     update_node<Topo, MODE, TERMS, BLOCK>(cc, sh, s_pb, tid, 1, x, v, coef, rng);
     NodeTrig<A> cur = node_trig<HW, A>(x);
 #pragma unroll
     for (int k = 1; k <= J; ++k) {
-        if (k > 1) progress_prio<J, 2>(k);
+        if (k > 1) progress_prio<J, 1, IKPSO_PRIO_LEVELS_4WAVE>(k);
         NodeTrig<A> nxt = cur;
         if (k < J) {
             update_node<Topo, MODE, TERMS, BLOCK>(cc, sh, s_pb, tid, k + 1, x, v, coef, rng);
