@@ -29,7 +29,7 @@ sys.path.insert(0, str(ROOT / "inverse-kinematics-pso-research_amd"))
 # MI355X constants (MI355X_MICROARCH.md "Chip-level parameters")
 HBM_PEAK_GBS = 8000.0
 CUS, SIMDS, LANES_PER_CLK, CLOCK_GHZ = 256, 4, 32, 2.4
-VALU_PEAK_TINSTR = CUS * SIMDS * LANES_PER_CLK * CLOCK_GHZ / 1e3  # lane-instructions/s, 78.6 T
+VALU_PEAK_TINSTR = CUS * SIMDS * LANES_PER_CLK * CLOCK_GHZ / 1e3  # VALU lane-instructions/s, 78.6 T
 # algorithmic bytes per particle-update = 20*D + 8 (x, v, pbest read; x, v written; pbest
 # fitness r/w): 428 B at D = 21, 1208 B at D = 60
 
@@ -53,6 +53,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU baseline sample (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="CPU baseline threads (0 = every CPU in this process's affinity mask)")
+    ap.add_argument("--reference-steps", type=int, default=3,
+                    help="after the FAST legs, time this many steps of the same workload in REFERENCE arithmetic "
+                         "(the bit-exact path; rank 0, configs 3/4; 0 = skip)")
     ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
                     help="gloo: rehearse the N>1 path with ranks sharing the visible GPUs (not a measurement)")
     return ap.parse_args()
@@ -302,6 +305,33 @@ def main():
         single_ms = 1e3 * float(np.median(ts))
         s2.close()
 
+    # the REFERENCE-arithmetic (bit-identical to the oracle) throughput of the same workload, driver-measured
+    reference_arith = None
+    if rank == 0 and args.arith == "fast" and args.reference_steps > 0 and cfg in (3, 4):
+        sr = ikpso.BatchSolver(wl.chain, P, pso=ikpso.PSOConfig(0.5, 0.5, 1.25, I), fit=wl.fit, arith="reference",
+                               kernel=args.kernel)
+        sr.seed(Bl, seed_base=0, first_swarm=first)
+        out_r = (torch.empty((Bl, D), device=dev), torch.empty((Bl,), device=dev), torch.empty((Bl,), device=dev))
+        sr.solve(targets, iterations=I, out=out_r)
+        torch.cuda.synchronize()
+        evr = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+               for _ in range(args.reference_steps)]
+        tr = time.perf_counter()
+        for a, b in evr:
+            a.record()
+            sr.solve(targets, iterations=I, out=out_r)
+            b.record()
+        torch.cuda.synchronize()
+        el_r = time.perf_counter() - tr
+        reference_arith = {"value": Bl * P * I * args.reference_steps / el_r, "unit": "particle-updates/s",
+                           "kernel_ms": round(float(np.mean([a.elapsed_time(b) for a, b in evr])), 3),
+                           "steps": args.reference_steps, "warmup": 1, "kernel": sr.kernel,
+                           "swarms": Bl, "check_finite": bool(torch.isfinite(out_r[1]).all()),
+                           "note": "REFERENCE arithmetic: the reference's 4x4 operation order, no FMA contraction, "
+                                   "correctly rounded sin/cos -- bit-identical to the CPU oracle "
+                                   "(tests/test_gpu_parity.py), same workload, rank 0"}
+        sr.close()
+
     if rank == 0:
         ups_launch = Bl * P * I
         kern_s = kern_ms / 1e3
@@ -310,27 +340,35 @@ def main():
         streaming = "streaming" in solver.kernel
         vpu = None if streaming else valu_per_update(solver.kernel)
         valu = None
+        lib_id = ikpso.build_id()
         if vpu:
-            # issue slots: one slot = the 2 SIMD cycles an ordinary wave64 op occupies.  gfx950 issue costs are
-            # not uniform (tools/probes/valu_probe.hip, profiles/r02/valu_issue_costs.txt): v_lshlrev, v_add3,
-            # v_cvt, v_med3/max3 ... occupy 4.1 cycles, v_sin/v_cos 8.1.  The committed issue model
-            # (tools/issue_model.py on the kernel's ISA) gives the hot loop's mean cycles per VALU instruction;
-            # times the counter-measured instructions per update that is the slots each update occupies.
+            # VALU lane-instructions per update (rocprofv3 SQ_INSTS_VALU x 64 / updates, committed in
+            # profiles/valu_per_update.json) x the live update rate, against the chip's 78.6 T lane-instructions/s
+            # (256 CU x 4 SIMD x 32 lanes x 2.4 GHz: every wave64 VALU op at its 2-cycle full rate).
+            instr = vpu["valu_lane_instr_per_update"]
+            ach = ups_launch * instr / kern_s / 1e12
+            # Secondary views.  gfx950 issue costs are not uniform (tools/probes/valu_probe.hip,
+            # profiles/r02/valu_issue_costs.txt): v_lshlrev, v_add3, v_cvt, v_med3/max3 ... occupy 4.1 cycles,
+            # v_sin/v_cos 8.1; the issue model (tools/issue_model.py on the kernel's ISA) prices the hot loop
+            # opcode by opcode -- a roof lowered to the kernel's own instruction mix, not the chip's.
             trans = vpu.get("trans_lane_instr_per_update") or 0.0
             model = vpu.get("issue_model")
-            slots_simple = vpu["valu_lane_instr_per_update"] + 3.0 * trans
-            slots = vpu["valu_lane_instr_per_update"] * model["mean_cycles_per_instr"] / 2.0 if model else slots_simple
-            ach = ups_launch * slots / kern_s / 1e12
-            valu = {"achieved": round(ach, 2), "peak": round(VALU_PEAK_TINSTR, 1), "unit": "Tlane-slot/s",
+            slots_simple = instr + 3.0 * trans
+            slots = instr * model["mean_cycles_per_instr"] / 2.0 if model else None
+            valu = {"achieved": round(ach, 2), "peak": round(VALU_PEAK_TINSTR, 1), "unit": "Tlane-instr/s",
                     "frac": round(ach / VALU_PEAK_TINSTR, 4),
-                    "instr_per_update": vpu["valu_lane_instr_per_update"], "trans_per_update": trans,
-                    "issue_slots_per_update": round(slots, 1), "source": vpu.get("source"),
-                    "issue_model": model,
+                    "instr_per_update": instr, "trans_per_update": trans, "source": vpu.get("source"),
+                    "measured_on_build": vpu.get("build_id"), "stale": vpu.get("build_id") != lib_id,
+                    "frac_issue_model": round(ups_launch * slots / kern_s / 1e12 / VALU_PEAK_TINSTR, 4)
+                    if slots else None,
+                    "issue_slots_per_update": round(slots, 1) if slots else None, "issue_model": model,
                     "frac_uniform_cost": round(ups_launch * slots_simple / kern_s / 1e12 / VALU_PEAK_TINSTR, 4),
-                    "note": "VALU issue roof: 78.6 T lane-slots/s = 256 CU x 4 SIMD x 32 lanes x 2.4 GHz (one "
-                            "slot = 2 SIMD cycles); slots per update = SQ_INSTS_VALU lane-instructions per update x "
-                            "the hot loop's mean measured issue cost / 2 (frac_uniform_cost: every op 1 slot, "
-                            "transcendentals 4)"}
+                    "note": "frac = SQ_INSTS_VALU lane-instructions per update x updates/s / 78.6 T (chip peak, "
+                            "every op at full rate); frac_issue_model: the same time priced at each opcode's "
+                            "measured gfx950 issue cost (4-cycle integer/convert/med3 forms, 8-cycle sin/cos) -- "
+                            "the fraction of the SIMDs' issue cycles the kernel's own mix keeps busy; "
+                            "frac_uniform_cost: transcendentals as 4 slots. stale: the counters were measured on "
+                            "another build than the loaded library"}
         # the streaming kernels move x/v/pbest through HBM (HBM-bound); an on-chip kernel without a committed
         # PMC profile is reported unmeasured rather than against the HBM formulation it does not use
         on_chip_unmeasured = not streaming and not valu
@@ -342,6 +380,7 @@ def main():
             "frac": valu["frac"] if valu else (None if on_chip_unmeasured else round(alg_gbs / HBM_PEAK_GBS, 4)),
             "traffic": round(vpu["hbm_bytes_per_update"] * ups_launch) if vpu else None,
             "kernel": solver.kernel + (" (I+2 launches per batch)" if streaming else " (one launch = one batch)"),
+            "stale": bool(valu and valu["stale"]),
             "kernel_ms": round(kern_ms, 3),
             "hbm_measured": None if not vpu else {
                 "achieved": round(ups_launch * vpu["hbm_bytes_per_update"] / kern_s / 1e9, 2),
@@ -392,7 +431,9 @@ def main():
             "solves_per_s": total * args.steps / elapsed,
             "single_solve_ms": single_ms,
             "roofline": roofline,
+            "reference_arith": reference_arith,
             "cpu_baseline": cpu,
+            "build_id": lib_id,
             "check": {"finite": finite, "mean_fitness": mean_fit, "mean_residual": mean_res},
             "parity": f"{args.arith.upper()} arithmetic. REFERENCE mode is bit-identical to the CPU oracle "
                       "(tests/test_gpu_parity.py); FAST (benchmarked) holds FK |dp| <= 2e-5, tier A |dtheta| <= 1e-4, "

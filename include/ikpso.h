@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define IKPSO_ABI_VERSION 4
+#define IKPSO_ABI_VERSION 5
 
 typedef int ikpso_status;
 enum {
@@ -104,7 +104,10 @@ enum {
 
 /* Arithmetic mode of the device kernels. */
 enum {
-    IKPSO_ARITH_FAST = 0,      /* closed-form 3x3 FK, FMA contraction (default) */
+    IKPSO_ARITH_FAST = 0,      /* closed-form 3x3 FK, FMA contraction (default); sin/cos on the
+                                  transcendental unit when every clamp bound and rest angle of the
+                                  chain lies within +-100 rad (the answers are clamped there), else a
+                                  1-ulp polynomial */
     IKPSO_ARITH_REFERENCE = 1  /* the reference's 4x4 operation order, no FMA contraction */
 };
 
@@ -240,6 +243,14 @@ ikpso_status ikpso_solver_evaluate(ikpso_solver* solver, const float* angles, co
                                    const float* rest, int64_t n, float* out_fitness, float* out_positions,
                                    void* stream);
 
+/* Copy the generator states of local swarms [first_swarm, first_swarm + count)
+ * (P states each, swarm-major, 48-byte curandState layout) into dst (any memory,
+ * count * P states), after settling a pending solve (ABI >= 5).  Synchronises
+ * `stream`.  The parity tests compare them with the oracle's: the draw count of
+ * every particle (D at init, 3 D per iteration) is integer work, bit-exact. */
+ikpso_status ikpso_solver_generator_states(ikpso_solver* solver, int64_t first_swarm, int64_t count, void* dst,
+                                           void* stream);
+
 /* Introspection.  dof = D, the free dimensions. */
 int ikpso_solver_dof(const ikpso_solver* solver);
 int ikpso_solver_effectors(const ikpso_solver* solver);
@@ -249,6 +260,10 @@ int ikpso_solver_effectors(const ikpso_solver* solver);
 const char* ikpso_solver_kernel_name(const ikpso_solver* solver);
 
 int ikpso_abi_version(void);
+/* Hash of the sources the library was built from (csrc/ *.h *.hip *.cpp Makefile,
+ * include/ *.h; ABI >= 5), plus "+" and a hash of the extra compiler flags of a
+ * variant build.  The Python loader compares it with the tree it runs from. */
+const char* ikpso_build_id(void);
 const char* ikpso_status_string(ikpso_status status);
 int ikpso_last_hip_error(void);
 

@@ -19,6 +19,9 @@
 
 using namespace ikpso;
 
+// csrc/_build/ikpso_build_id.cpp, written by the Makefile on every build
+extern "C" const char ikpso_build_id_string[];
+
 static_assert(sizeof(ikpso_node) == 88, "ikpso_node must match NodeCUDA (88 bytes)");
 static_assert(sizeof(ikpso_rng_state) == 48, "ikpso_rng_state must match curandStateXORWOW (48 bytes)");
 static_assert(sizeof(ikpso_pso_config) == 16, "PSOConfig is 16 bytes");
@@ -304,6 +307,12 @@ ikpso_status parse_chain(const std::vector<ikpso_node>& nodes, const ikpso_pso_c
             ch.aux[7 * J + d] = fr ? ex.soft_hi[r] : INFINITY;
             r += fr;
         }
+    // the transcendental unit's range (kHwTrigMaxAbs): every evaluated angle is
+    // clamped to [lo, hi] after the first update, the warm start is the rest pose
+    for (int d = 0; d < 3 * J && d < 64; ++d)
+        if ((ch.free_mask >> d) & 1)
+            ch.poly_trig = ch.poly_trig || !(fabsf(ch.lo[d]) <= kHwTrigMaxAbs) || !(fabsf(ch.hi[d]) <= kHwTrigMaxAbs) ||
+                           !(fabsf(ch.rest[d]) <= kHwTrigMaxAbs);
     if (!chain_supported(ch)) return IKPSO_ERR_UNSUPPORTED;
     return IKPSO_OK;
 }
@@ -321,7 +330,7 @@ constexpr int kDHMin = 3, kDHMax = 12;
 bool build_dh(const std::vector<ikpso_node>& nodes, const ChainHost& eu, const Extras& ex, ChainHost& dh)
 {
     const int J = eu.J, N = eu.dfree;
-    if (eu.topo != TopoKind::SerialTip || eu.use_posref || eu.num_coll > 0 || !eu.masked) return false;
+    if (eu.topo != TopoKind::SerialTip || eu.use_posref || eu.num_coll > 0 || !eu.masked || eu.poly_trig) return false;
     if (N < kDHMin || N > kDHMax) return false;
     const ikpso_node& o = nodes[0];
     D3 g = d3_mul(d3_mul(d3_rot(0, o.rotation[0]), d3_rot(1, o.rotation[1])), d3_rot(2, o.rotation[2]));
@@ -510,8 +519,14 @@ bool prefer_latency_coop(const ChainHost& ch, int mode, int P, int64_t B)
 // forces the give-up path so the fallback can be tested).
 uint32_t coop_spin_limit()
 {
+    // only an explicit decimal number overrides the default: an empty or
+    // malformed value (which strtoul would read as 0, the give-up path) is ignored
     const char* e = getenv("IKPSO_COOP_SPIN_LIMIT");
-    return e ? (uint32_t)strtoul(e, nullptr, 10) : kCoopSpinLimit;
+    if (!e || !*e) return kCoopSpinLimit;
+    char* end = nullptr;
+    const unsigned long v = strtoul(e, &end, 10);
+    if (end == e || *end != '\0' || v > 0xFFFFFFFFul) return kCoopSpinLimit;
+    return (uint32_t)v;
 }
 
 // Point the coop fields of `io` into workspace `ws` (coop_workspace_bytes) and
@@ -522,7 +537,6 @@ hipError_t carve_coop(SwarmIO& io, void* ws, int G, int NG, int block, int D, hi
     Carver cv{static_cast<char*>(ws)};
     io.coop_error = cv.take<int32_t>(1);
     io.coop_slots = cv.take<unsigned long long>((size_t)NG * 2 * G * kCoopSlot(D));
-    io.coop_pbest = coop_global_pbest(D) ? cv.take<float>((size_t)NG * G * D * block) : nullptr;
     io.coop_timing = IKPSO_COOP_TIMING ? cv.take<unsigned long long>((size_t)NG * G * 4) : nullptr;
     io.coop_g = G;
     io.coop_ng = NG;
@@ -576,8 +590,6 @@ struct ikpso_solver {
     // kernels if a group could not assemble.
     ikpso_rng_state* rng_snap = nullptr;
     int64_t snap_capacity = 0;
-    void* ws_fallback = nullptr;
-    size_t ws_fallback_bytes = 0;
     struct {
         bool active = false;
         const float* targets = nullptr;
@@ -636,6 +648,8 @@ ikpso_status solve_streaming(ikpso_solver* s, void** ws, size_t* ws_bytes, const
 extern "C" {
 
 int ikpso_abi_version(void) { return IKPSO_ABI_VERSION; }
+
+const char* ikpso_build_id(void) { return ikpso_build_id_string; }
 
 int ikpso_last_hip_error(void) { return g_last_hip_error; }
 
@@ -888,20 +902,26 @@ ikpso_status ikpso_solver_create(const ikpso_solver_desc* desc, ikpso_solver** o
 ikpso_status ikpso_solver_destroy(ikpso_solver* s)
 {
     if (!s) return IKPSO_OK;
+    // a pending cooperative solve still runs on the buffers freed below: settle it
+    // (its fallback, if it needs one, completes the caller's outputs)
+    const ikpso_status pend = s->pending.active ? ikpso_solver_sync(s) : IKPSO_OK;
     if (s->rng) (void)hipFree(s->rng);
     if (s->rng_snap) (void)hipFree(s->rng_snap);
-    if (s->ws_fallback) (void)hipFree(s->ws_fallback);
     if (s->aux) (void)hipFree(s->aux);
     if (s->aux_dh) (void)hipFree(s->aux_dh);
     if (s->ws) (void)hipFree(s->ws);
     delete s;
-    return IKPSO_OK;
+    return pend;
 }
 
 ikpso_status ikpso_solver_seed(ikpso_solver* s, int64_t capacity, uint64_t seed_base, int64_t first_swarm,
                                void* stream)
 {
     if (!s || capacity < 0 || first_swarm < 0) return IKPSO_ERR_INVALID_ARG;
+    if (s->pending.active) {  // settle the last cooperative solve before its states are replaced
+        const ikpso_status st = ikpso_solver_sync(s);
+        if (st != IKPSO_OK) return st;
+    }
     if (capacity > s->capacity) {
         if (s->rng) IKPSO_HIP(hipFree(s->rng));
         s->rng = nullptr;
@@ -1022,9 +1042,10 @@ ikpso_status ikpso_solver_sync(ikpso_solver* s)
     // generator states and solve the whole batch on the streaming kernels.
     IKPSO_HIP(hipMemcpyAsync(s->rng, s->rng_snap, sizeof(ikpso_rng_state) * (size_t)p.num_swarms * s->P,
                              hipMemcpyDeviceToDevice, p.stream));
-    const ikpso_status st = solve_streaming(s, &s->ws_fallback, &s->ws_fallback_bytes, p.targets, p.start_pose,
-                                            p.num_swarms, p.iterations, p.out_angles, p.out_fitness, p.out_residual,
-                                            p.stream);
+    // the cooperative workspace is idle now (the launch has completed): the
+    // streaming solve runs in it, grown as needed, so no second workspace is held
+    const ikpso_status st = solve_streaming(s, &s->ws, &s->ws_bytes, p.targets, p.start_pose, p.num_swarms,
+                                            p.iterations, p.out_angles, p.out_fitness, p.out_residual, p.stream);
     if (st != IKPSO_OK) return st;
     IKPSO_HIP(hipStreamSynchronize(p.stream));
     ++s->fallbacks;
@@ -1033,6 +1054,22 @@ ikpso_status ikpso_solver_sync(ikpso_solver* s)
 }
 
 int64_t ikpso_solver_fallbacks(const ikpso_solver* s) { return s ? s->fallbacks : 0; }
+
+ikpso_status ikpso_solver_generator_states(ikpso_solver* s, int64_t first_swarm, int64_t count, void* dst, void* stream)
+{
+    if (!s || first_swarm < 0 || count < 0 || (count > 0 && !dst) || first_swarm + count > s->capacity)
+        return IKPSO_ERR_INVALID_ARG;
+    if (s->pending.active) {
+        const ikpso_status st = ikpso_solver_sync(s);
+        if (st != IKPSO_OK) return st;
+    }
+    if (count == 0) return IKPSO_OK;
+    const hipStream_t hs = (hipStream_t)stream;
+    IKPSO_HIP(hipMemcpyAsync(dst, s->rng + (size_t)first_swarm * s->P, sizeof(ikpso_rng_state) * (size_t)count * s->P,
+                             hipMemcpyDefault, hs));
+    IKPSO_HIP(hipStreamSynchronize(hs));
+    return IKPSO_OK;
+}
 
 int64_t ikpso_coop_fallbacks(void) { return g_coop_fallbacks.load(); }
 

@@ -79,42 +79,8 @@ struct CoopShared {
 // chunks, reduce; returns the group-wide minimum key of this exchange (uniform)
 // and leaves the winner's local best in sh.g when it improves on `gkey` (or
 // always when `force`).  Called by every wave; wave 0 does the global work.
-// One chunk's local-best plane [d][lane] in global memory (coop_global_pbest):
-// a buffer resource, so an access costs one VGPR offset (the lane) and an SGPR
-// offset (the dimension) instead of a 64-bit address per dimension.
-struct PbPlane {
-    __amdgpu_buffer_rsrc_t rsrc;
-    uint32_t voff;
-    __device__ __forceinline__ PbPlane(float* base, int D, int block, int lane)
-        : rsrc(__builtin_amdgcn_make_buffer_rsrc(base, 0, D * block * 4, 0x00020000)), voff((uint32_t)lane * 4u)
-    {
-    }
-    template <int BLOCK>
-    __device__ __forceinline__ float ld(int d) const
-    {
-        return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsrc, (int)voff, d * BLOCK * 4, 0));
-    }
-    template <int BLOCK>
-    __device__ __forceinline__ void st(int d, float v) const
-    {
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rsrc, (int)voff, d * BLOCK * 4, 0);
-    }
-};
-
-// The winner's local best: from the LDS array [d][lane] or the global plane.
-template <int BLOCK>
-__device__ __forceinline__ float local_best(const float* s_pb, int d, int lane)
-{
-    return s_pb[d * BLOCK + lane];
-}
-template <int BLOCK>
-__device__ __forceinline__ float local_best(const PbPlane& pb, int d, int lane)
-{
-    return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(pb.rsrc, lane * 4, d * BLOCK * 4, 0));
-}
-
-template <class Topo, int BLOCK, class PB>
-__device__ __forceinline__ void coop_exchange(SwarmShared<Topo>& sh, CoopShared<Topo::J>& cs, const PB& s_pb,
+template <class Topo, int BLOCK>
+__device__ __forceinline__ void coop_exchange(SwarmShared<Topo>& sh, CoopShared<Topo::J>& cs, const float* s_pb,
                                               uint32_t local_key, int32_t* error, uint32_t spin_limit, bool force)
 {
     constexpr int D = Topo::D;
@@ -122,18 +88,6 @@ __device__ __forceinline__ void coop_exchange(SwarmShared<Topo>& sh, CoopShared<
     static_assert(D + 1 <= 64, "wave 0 publishes the record in one store instruction");
     int lidx;
     const uint32_t lmin = swarm_argmin(sh, 0, local_key, &lidx);  // one workgroup barrier inside
-#if IKPSO_COOP_NO_EXCHANGE  // timing-only ablation: every chunk its own swarm (no cross-CU hand-off)
-    if (wave_id() == 0) {
-        const int lane = lane_id_here();
-        if (force || lmin < cs.gkey) {
-            if (lane < D) sh.g[lane] = local_best<BLOCK>(s_pb, lane, lidx);
-            if (lane == 0) cs.gkey = lmin;
-        }
-        (void)error, (void)spin_limit, (void)SLOT;
-    }
-    __syncthreads();
-    return;
-#endif
     if (wave_id() == 0) {
         compiler_fence();
 #if IKPSO_COOP_TIMING
@@ -145,7 +99,7 @@ __device__ __forceinline__ void coop_exchange(SwarmShared<Topo>& sh, CoopShared<
         const granule_t tag = (granule_t)(e + 1) << 32;
         granule_t* base = cs.slots + (size_t)(e & 1) * G * SLOT;
         // granule 0: the key; granules 1..D: the chunk winner's local best
-        const float mine_d = lane >= 1 && lane <= D ? local_best<BLOCK>(s_pb, lane - 1, lidx) : 0.0f;
+        const float mine_d = lane >= 1 && lane <= D ? s_pb[(lane - 1) * BLOCK + lidx] : 0.0f;
         if (lane <= D) st_granule(base + (size_t)member * SLOT + lane, tag | (lane == 0 ? lmin : __float_as_uint(mine_d)));
         // the G key granules, in chunk order (lanes 0..G-1; G <= 64)
         uint32_t n = 0;
@@ -192,93 +146,6 @@ __device__ __forceinline__ void coop_exchange(SwarmShared<Topo>& sh, CoopShared<
     __syncthreads();
 }
 
-#ifndef IKPSO_COOP_SHL1_ADD
-#define IKPSO_COOP_SHL1_ADD 0  // the add-for-shift generator form in the throughput build too
-#endif
-#ifndef IKPSO_PBG_HW
-#define IKPSO_PBG_HW 1        // FAST sin/cos on the transcendental unit in the long-chain build
-#endif
-#ifndef IKPSO_PBG_AHEAD
-#define IKPSO_PBG_AHEAD 2     // nodes of local bests loaded ahead of their use
-#endif
-#ifndef IKPSO_PBG_V_AHEAD
-#define IKPSO_PBG_V_AHEAD 1   // nodes of velocities read from LDS ahead of their use
-#endif
-
-// One PSO iteration of the long-chain build: positions in VGPRs, velocities in
-// LDS (s_v[d][lane]), local bests in the chunk's global plane, loaded
-// IKPSO_PBG_AHEAD nodes ahead.  Same arithmetic and draw order as swarm_step.
-template <class Topo, int MODE, int TERMS, int BLOCK, class Rng>
-__device__ __forceinline__ void swarm_step_pbg(const ChainConsts<Topo::J>& cc, SwarmShared<Topo>& sh, float* s_v,
-                                               const PbPlane& pb, int tid, float (&x)[Topo::D], float& pbf,
-                                               const PsoCoef& coef, Rng& rng)
-{
-    constexpr int J = Topo::J, A = Topo::A, D = Topo::D;
-    constexpr bool MASK = kMasked<Topo, TERMS>;
-    constexpr bool HW = IKPSO_PBG_HW && IKPSO_SINCOS_HW && MODE == IKPSO_ARITH_FAST && !(TERMS & kTermColliders);
-    constexpr int AH = (IKPSO_PBG_AHEAD < J) ? IKPSO_PBG_AHEAD : J;
-    constexpr int VH = (IKPSO_PBG_V_AHEAD < J) ? IKPSO_PBG_V_AHEAD : J;
-    FitnessFor<Topo, MODE, TERMS> acc(cc, sh.dh, sh.soft);
-    float ring[AH + 1][A], vring[VH + 1][A];
-#pragma unroll
-    for (int n = 0; n < AH; ++n)
-#pragma unroll
-        for (int ax = 0; ax < A; ++ax) ring[n][ax] = pb.template ld<BLOCK>(A * n + ax);
-#pragma unroll
-    for (int n = 0; n < VH; ++n)
-#pragma unroll
-        for (int ax = 0; ax < A; ++ax) vring[n][ax] = s_v[(A * n + ax) * BLOCK + tid];
-#pragma unroll
-    for (int k = 1; k <= J; ++k) {
-        const int cs = (k - 1) % (AH + 1), cv = (k - 1) % (VH + 1);
-        float cpb[A], cvel[A];
-#pragma unroll
-        for (int ax = 0; ax < A; ++ax) {
-            cpb[ax] = ring[cs][ax];
-            cvel[ax] = vring[cv][ax];
-        }
-        if (k - 1 + AH < J) {
-            const int nn = k - 1 + AH, ns = nn % (AH + 1);
-#pragma unroll
-            for (int ax = 0; ax < A; ++ax) ring[ns][ax] = pb.template ld<BLOCK>(A * nn + ax);
-        }
-        if (k - 1 + VH < J) {
-            const int nn = k - 1 + VH, ns = nn % (VH + 1);
-#pragma unroll
-            for (int ax = 0; ax < A; ++ax) vring[ns][ax] = s_v[(A * nn + ax) * BLOCK + tid];
-        }
-#pragma unroll
-        for (int ax = 0; ax < A; ++ax) {
-            const int d = A * (k - 1) + ax;
-            if (MASK && !dim_free(cc, d)) continue;  // locked: stays at rest
-            float vv = cvel[ax];
-            pso_update<MODE>(x[d], vv, cpb[ax], sh.g[d], coef, rng);
-            s_v[d * BLOCK + tid] = vv;
-            if constexpr (TERMS & kTermUniformBounds)
-                x[d] = clamp_mode<MODE>(x[d], cc.lo[0], cc.hi[0]);
-            else
-                x[d] = clamp_mode<MODE>(x[d], sh.lo[d], sh.hi[d]);
-        }
-        float rest[A], tgt[3];
-#pragma unroll
-        for (int ax = 0; ax < A; ++ax) rest[ax] = sh.rest[A * (k - 1) + ax];
-#pragma unroll
-        for (int c = 0; c < 3; ++c) tgt[c] = Topo::effector(k) ? sh.tgt[3 * (k - 1) + c] : 0.0f;
-        if constexpr (MODE == IKPSO_ARITH_FAST)
-            acc.node_trig(cc, k, x + A * (k - 1), node_trig<HW, A>(x + A * (k - 1)), rest, tgt, nullptr);
-        else
-            acc.node(cc, k, x + A * (k - 1), rest, tgt, nullptr);
-        __builtin_amdgcn_sched_barrier(0);
-    }
-    // updateLocalBests (src/kernel.cu:202-221): strict improvement
-    const float f = acc.finish(cc);
-    if (f < pbf) {
-        pbf = f;
-#pragma unroll
-        for (int d = 0; d < D; ++d) pb.template st<BLOCK>(d, x[d]);
-    }
-}
-
 // BLOCK: kCoopThreads<D>() (throughput: fill each CU), or kCoopLatencyThreads
 // for a few swarms (latency: one wave per SIMD on 4x more CUs).
 template <class Topo, int MODE, int TERMS, int BLOCK>
@@ -287,19 +154,16 @@ __global__ void __launch_bounds__(BLOCK, (BLOCK >= 256 ? BLOCK / 256 : 1))
 {
     constexpr int J = Topo::J;
     constexpr int D = Topo::D;
-    constexpr bool PBG = coop_global_pbest(D);
     const int tid = threadIdx.x;
     const int P = io.P;
 
-    // local bests [d][lane] (PBG: the velocities; the local bests are in the
-    // chunk's global plane); padded to > 80 KiB so a CU never holds two
+    // local bests [d][lane]; padded to > 80 KiB so a CU never holds two
     // workgroups (the launch geometry assumes one per CU)
     constexpr int kPb = (D * BLOCK * 4 > 82 * 1024) ? D * BLOCK : 82 * 1024 / 4;
     __shared__ SwarmLds<Topo, kPb, CoopShared<J>> lds;
     SwarmShared<Topo>& sh = lds.sh;
     CoopShared<J>& cs = lds.extra;
     float* const s_pb = lds.pb;
-    const PbPlane pbg(PBG ? io.coop_pbest + (size_t)blockIdx.x * D * BLOCK : nullptr, D, BLOCK, tid);
     if (tid == 0) {
         // XCD-aware group membership: workgroups b, b+8, b+16, ... share an XCD
         const int G = io.coop_g;
@@ -323,33 +187,19 @@ __global__ void __launch_bounds__(BLOCK, (BLOCK >= 256 ? BLOCK / 256 : 1))
         stage_swarm_inputs<Topo>(cc, io.targets, io.start_pose, b, sh);
         // the add-for-shift issue form only in the latency variant (one wave per
         // SIMD, room to spare): in the 2-wave serial-20 kernel it cost 5 %
-        using Rng = XorwowT<(IKPSO_COOP_SHL1_ADD || BLOCK == kCoopLatencyThreads) &&
-                            std::is_same_v<RngFor<TERMS>, XorwowT<true>>>;
+        using Rng = XorwowT<BLOCK == kCoopLatencyThreads && std::is_same_v<RngFor<TERMS>, XorwowT<true>>>;
         Rng rng{0, 0, 0, 0, 0, 0};
         if (i < P) load_rng(rng, io.rng + b * P + i);
         if (tid == 0) cs.gkey = 0xFFFFFFFFu;
         __syncthreads();
 
         // initParticlesKernel + initLocalBests (src/kernel.cu:191-266)
-        float x[D], v[PBG ? 1 : D];
-        if constexpr (PBG) {
-#pragma unroll
-            for (int d = 0; d < D; ++d) {
-                x[d] = sh.rest[d];
-                const bool locked = kMasked<Topo, TERMS> && !dim_free(cc, d);
-                s_pb[d * BLOCK + tid] = locked ? 0.0f : __builtin_fmaf(rng.uniform(), 2.0f, -1.0f);
-                pbg.template st<BLOCK>(d, x[d]);
-            }
-        } else {
-            init_particle<Topo, TERMS, BLOCK>(cc, sh, s_pb, tid, x, v, rng);
-        }
+        float x[D], v[D];
+        init_particle<Topo, TERMS, BLOCK>(cc, sh, s_pb, tid, x, v, rng);
         float pbf = fitness<Topo, MODE, TERMS>(cc, x, sh.rest, sh.tgt, nullptr, sh.dh, sh.soft);
         // swarm argmin + unconditional first global-best copy (src/kernel.cu:297-304)
         const uint32_t key0 = i < P ? ordered_key(pbf) : 0xFFFFFFFFu;
-        if constexpr (PBG)
-            coop_exchange<Topo, BLOCK>(sh, cs, pbg, key0, io.coop_error, io.coop_spin_limit, true);
-        else
-            coop_exchange<Topo, BLOCK>(sh, cs, s_pb, key0, io.coop_error, io.coop_spin_limit, true);
+        coop_exchange<Topo, BLOCK>(sh, cs, s_pb, key0, io.coop_error, io.coop_spin_limit, true);
 
 #if IKPSO_COOP_TIMING
         unsigned long long t_step = 0, t_bar = 0, t_exch = 0, n_it = 0;
@@ -360,19 +210,13 @@ __global__ void __launch_bounds__(BLOCK, (BLOCK >= 256 ? BLOCK / 256 : 1))
 #if IKPSO_COOP_TIMING
             const unsigned long long t0 = __builtin_amdgcn_s_memtime();
 #endif
-            if constexpr (PBG)
-                swarm_step_pbg<Topo, MODE, TERMS, BLOCK>(cc, sh, s_pb, pbg, tid, x, pbf, coef, rng);
-            else
-                swarm_step<Topo, MODE, TERMS, BLOCK>(cc, sh, s_pb, tid, x, v, pbf, coef, rng);
+            swarm_step<Topo, MODE, TERMS, BLOCK>(cc, sh, s_pb, tid, x, v, pbf, coef, rng);
             const bool act = cs.member * BLOCK + tid < P;
             const uint32_t key = act ? ordered_key(pbf) : 0xFFFFFFFFu;
 #if IKPSO_COOP_TIMING
             const unsigned long long t1 = __builtin_amdgcn_s_memtime();
 #endif
-            if constexpr (PBG)
-                coop_exchange<Topo, BLOCK>(sh, cs, pbg, key, io.coop_error, io.coop_spin_limit, false);
-            else
-                coop_exchange<Topo, BLOCK>(sh, cs, s_pb, key, io.coop_error, io.coop_spin_limit, false);
+            coop_exchange<Topo, BLOCK>(sh, cs, s_pb, key, io.coop_error, io.coop_spin_limit, false);
 #if IKPSO_COOP_TIMING
             const unsigned long long t2 = __builtin_amdgcn_s_memtime();
             t_step += t1 - t0;  // wave 0's own step
@@ -413,13 +257,8 @@ __global__ void __launch_bounds__(BLOCK, (BLOCK >= 256 ? BLOCK / 256 : 1))
 #pragma unroll
                 for (int d = 0; d < D; ++d) {
                     base[(int64_t)d * P + ii] = x[d];
-                    if constexpr (PBG) {
-                        base[(int64_t)(D + d) * P + ii] = s_pb[d * BLOCK + tid];
-                        base[(int64_t)(2 * D + d) * P + ii] = pbg.template ld<BLOCK>(d);
-                    } else {
-                        base[(int64_t)(D + d) * P + ii] = v[d];
-                        base[(int64_t)(2 * D + d) * P + ii] = s_pb[d * BLOCK + tid];
-                    }
+                    base[(int64_t)(D + d) * P + ii] = v[d];
+                    base[(int64_t)(2 * D + d) * P + ii] = s_pb[d * BLOCK + tid];
                 }
             }
             if (io.dump_bests) io.dump_bests[bb * P + ii] = pbf;

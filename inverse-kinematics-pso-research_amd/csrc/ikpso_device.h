@@ -18,41 +18,12 @@
 #include "ikpso_collide.h"
 #include "ikpso_params.h"
 
-#ifndef IKPSO_SINCOS_V2
-#define IKPSO_SINCOS_V2 1
-#endif
-#ifndef IKPSO_FK_SEQ
-#define IKPSO_FK_SEQ 1
-#endif
-#ifndef IKPSO_CLAMP_MED3
-#define IKPSO_CLAMP_MED3 1
-#endif
-#ifndef IKPSO_SCHED_NODE
-#define IKPSO_SCHED_NODE 0
-#endif
-#ifndef IKPSO_SCHED_DIM
-#define IKPSO_SCHED_DIM 1
-#endif
 // gfx950 VALU issue costs (tools/probes/valu_probe.hip, 4 waves per SIMD):
 // a wave64 v_add_u32 / v_xor_b32 / v_bitop3_b32 / v_fma_f32 on VGPR, inline or
 // literal operands issues every ~2.1-2.5 cycles per SIMD, but every
 // v_lshlrev_b32 and every VALU op that reads an SGPR takes ~4.1.  So the
 // generator's t << 1 is issued as t + t.  (Holding the sincos sign mask or the
 // PSO coefficients in VGPRs instead of SGPRs measured no better: DESIGN.md.)
-#ifndef IKPSO_ISSUE_SHL1_ADD
-#define IKPSO_ISSUE_SHL1_ADD 1
-#endif
-
-// FAST-mode sin/cos on the transcendental unit (v_sin_f32 / v_cos_f32) in the
-// kernels of chains up to 20 joints (D <= 60) that have no collider term; see
-// sincos_fast.
-#ifndef IKPSO_SINCOS_HW
-#define IKPSO_SINCOS_HW 1
-#endif
-#ifndef IKPSO_HW_TRIG_MAX_D
-#define IKPSO_HW_TRIG_MAX_D 60
-#endif
-
 
 namespace ikpso {
 
@@ -73,7 +44,7 @@ __host__ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32
 // the compiler, which would canonicalise an add back into the shift).
 __host__ __device__ __forceinline__ uint32_t shl1(uint32_t t)
 {
-#if defined(__HIP_DEVICE_COMPILE__) && IKPSO_ISSUE_SHL1_ADD
+#if defined(__HIP_DEVICE_COMPILE__)
     uint32_t r;
     asm("v_add_u32 %0, %1, %1" : "=v"(r) : "v"(t));
     return r;
@@ -107,7 +78,7 @@ __host__ __device__ __forceinline__ uint32_t as_uint(float f)
 
 // ---------------------------------------------------------------- XORWOW
 // cuRAND XORWOW restated: state {d, v[5]}; curand() and curand_uniform().
-// kAddShl: issue t << 1 as t + t (see IKPSO_ISSUE_SHL1_ADD; same bits).
+// kAddShl: issue t << 1 as t + t (shl1; same bits).
 template <bool kAddShl>
 struct XorwowT {
     uint32_t d, v0, v1, v2, v3, v4;
@@ -127,22 +98,12 @@ struct XorwowT {
     // result is the same single rounding.
     __host__ __device__ __forceinline__ float uniform()
     {
-#if IKPSO_ABL_NORNG  // timing-only ablation: no state advance
-        v4 += 0x9e3779b9u;
-        return __builtin_fmaf((float)v4, 2.3283064e-10f, 1.16415322e-10f);
-#else
         return __builtin_fmaf((float)next(), 2.3283064e-10f, 1.16415322e-10f);
-#endif
     }
     // c * uniform() with the scale folded in: fma(x, c*2^-32, c*2^-33).
     __host__ __device__ __forceinline__ float scaled(float q, float h)
     {
-#if IKPSO_ABL_NORNG
-        v4 += 0x9e3779b9u;
-        return __builtin_fmaf((float)v4, q, h);
-#else
         return __builtin_fmaf((float)next(), q, h);
-#endif
     }
 };
 using Xorwow = XorwowT<false>;
@@ -178,11 +139,6 @@ __host__ __device__ inline void xorwow_seed(uint64_t seed, uint32_t st[6])
 template <bool HW = false>
 __host__ __device__ __forceinline__ void sincos_fast(float x, float* s_out, float* c_out)
 {
-#if IKPSO_ABL_NOSIN  // timing-only ablation
-    *s_out = x * 0.5f;
-    *c_out = __builtin_fmaf(-0.5f, x, 1.0f);
-    return;
-#endif
 #if defined(__HIP_DEVICE_COMPILE__)
     if constexpr (HW) {
         // v_sin_f32 / v_cos_f32 on x / 2pi (revolutions; the transcendental unit
@@ -198,7 +154,6 @@ __host__ __device__ __forceinline__ void sincos_fast(float x, float* s_out, floa
         return;
     }
 #endif
-#if IKPSO_SINCOS_V2
     // Quadrant by the round-to-integer magic constant: k_big = x*2/pi + 1.5*2^23
     // holds q = rint(x*2/pi) in its low mantissa bits (one FMA instead of a
     // multiply, a rint and a float->int conversion); the swap of sin and cos
@@ -206,10 +161,6 @@ __host__ __device__ __forceinline__ void sincos_fast(float x, float* s_out, floa
     const float kb = __builtin_fmaf(x, 0.636619772367581343f, 12582912.0f);
     const float k = kb - 12582912.0f;
     const uint32_t qb = as_uint(kb);
-#else
-    const float k = __builtin_rintf(x * 0.636619772367581343f);
-    const int q = (int)k;
-#endif
     float r = __builtin_fmaf(-k, 1.57079637050628662109375f, x);
     r = __builtin_fmaf(-k, -4.37113900018624283e-8f, r);
     const float z = r * r;
@@ -219,7 +170,6 @@ __host__ __device__ __forceinline__ void sincos_fast(float x, float* s_out, floa
                               4.166664568298827e-2f);
     cp = __builtin_fmaf(cp, z, -0.5f);
     const float cv = __builtin_fmaf(cp, z, 1.0f);
-#if IKPSO_SINCOS_V2
 #if defined(__HIP_DEVICE_COMPILE__)
     const uint32_t m = (uint32_t)__builtin_amdgcn_sbfe((int)qb, 0, 1);  // q odd: all ones
     const uint32_t s1 = __builtin_amdgcn_bitop3_b32(m, as_uint(cv), as_uint(sv), 0xCA);  // m ? cv : sv
@@ -232,12 +182,6 @@ __host__ __device__ __forceinline__ void sincos_fast(float x, float* s_out, floa
     const uint32_t t = qb << 30;  // bit 31: q & 2 (sin sign); (q + 1) & 2 for cos
     *s_out = as_float(xor_sign(s1, t));
     *c_out = as_float(xor_sign(c1, t + 0x40000000u));
-#else
-    const bool swap = q & 1;
-    const uint32_t t = (uint32_t)q << 30;  // bit 31: q & 2 (sin sign); (q + 1) & 2 for cos
-    *s_out = as_float(xor_sign(as_uint(swap ? cv : sv), t));
-    *c_out = as_float(xor_sign(as_uint(swap ? sv : cv), t + 0x40000000u));
-#endif
 }
 
 // REFERENCE: the reduction and the polynomials (fdlibm __kernel_sin /
@@ -508,7 +452,7 @@ __device__ __forceinline__ Frame child_frame(const Frame& P, float a, float b, f
 {
     if constexpr (MODE == IKPSO_ARITH_REFERENCE)
         return child_frame_reference(P, a, b, c, len);
-    else if constexpr (SEQ && IKPSO_FK_SEQ)
+    else if constexpr (SEQ)
         return child_frame_fast_seq<HW>(P, a, b, c, len);
     else
         return child_frame_fast<HW>(P, a, b, c, len);
@@ -540,14 +484,13 @@ constexpr int kTermPosRef = 1, kTermPenalty = 2, kTermRuntime = 4, kTermUniformB
 // in the collider kernels, whose register allocation the opaque add perturbs
 // (spills); the draws are bit-identical either way.
 template <int TERMS>
-using RngFor = XorwowT<IKPSO_ISSUE_SHL1_ADD != 0 && !(TERMS & kTermColliders)>;
+using RngFor = XorwowT<!(TERMS & kTermColliders)>;
 
 // FAST sin/cos on the transcendental unit (sincos_fast<true>) for a kernel of
 // this topology and term set: chains that run 4 waves per SIMD, no collider term
 // (whose contact decisions the tests compare across kernels bit for bit).
 template <class Topo, int MODE, int TERMS>
-constexpr bool kHwTrig = IKPSO_SINCOS_HW && MODE == IKPSO_ARITH_FAST && !(TERMS & kTermColliders) &&
-                        Topo::D <= IKPSO_HW_TRIG_MAX_D;
+constexpr bool kHwTrig = MODE == IKPSO_ARITH_FAST && !(TERMS & kTermColliders) && Topo::D <= 60;
 
 // Which kernel builds honour ChainConsts::free_mask (the host routes masked
 // chains to them; the folded chain has no locked angles).
@@ -600,7 +543,7 @@ struct FitnessAcc {
     {
         static_assert(MODE == IKPSO_ARITH_FAST, "precomputed sin/cos: FAST arithmetic");
         const int pk = Topo::kGeneric ? cc.parent[k] : Topo::parent(k);
-        if (seq(k) && IKPSO_FK_SEQ)
+        if (seq(k))
             F[k] = child_frame_fast_seq_sc(F[pk], t.s[0], t.c[0], t.s[1], t.c[1], t.s[2], t.c[2], cc.len[k]);
         else
             F[k] = child_frame_fast_sc(F[pk], t.s[0], t.c[0], t.s[1], t.c[1], t.s[2], t.c[2], cc.len[k]);
@@ -651,8 +594,9 @@ struct FitnessAcc {
         }
         if constexpr (TERMS & kTermColliders) {
             // any node/link box hit -> FLT_MAX (the reference returns at the
-            // first hit; later nodes cannot change that)
-            if (!hit)
+            // first hit; later nodes cannot change that).  No colliders: a chain
+            // routed here for its polynomial sin/cos (ChainHost::poly_trig).
+            if (!hit && cc.num_coll > 0)
                 hit = node_collides(F[k].r00, F[k].r01, F[k].r02, F[k].r10, F[k].r11, F[k].r12, F[k].r20, F[k].r21,
                                     F[k].r22, F[k].px, F[k].py, F[k].pz, F[pk].px, F[pk].py, F[pk].pz, cc.len[k],
                                     cc.coll, cc.num_coll);
@@ -821,11 +765,8 @@ template <class Topo>
 struct IsSerialTip : std::false_type {};
 template <int J>
 struct IsSerialTip<TopoSerialTip<J>> : std::true_type {};
-#ifndef IKPSO_TIP_BACKWARD
-#define IKPSO_TIP_BACKWARD 1
-#endif
 template <class Topo, int MODE, int TERMS>
-constexpr bool kTipBackward = IKPSO_TIP_BACKWARD && MODE == IKPSO_ARITH_FAST &&
+constexpr bool kTipBackward = MODE == IKPSO_ARITH_FAST &&
                               (IsSerialTip<Topo>::value || Topo::kDH) &&
                               !(TERMS & (kTermPosRef | kTermRuntime | kTermColliders | kTermMask));
 
@@ -979,11 +920,6 @@ __device__ __forceinline__ float fitness(const ChainConsts<Topo::J>& cc, const f
 #pragma unroll
     for (int k = 1; k <= Topo::J; ++k) {
         acc.node(cc, k, x + A * (k - 1), rest + A * (k - 1), tgt + 3 * (k - 1), node_pos);
-#if IKPSO_SCHED_NODE
-        // One node at a time: keeps the scheduler from hoisting all 3J
-        // independent sincos evaluations to the top of the evaluation.
-        __builtin_amdgcn_sched_barrier(0);
-#endif
     }
     return acc.finish(cc);
 }
@@ -1065,14 +1001,6 @@ __device__ __forceinline__ void pso_update(float& x, float& v, float pb, float g
     }
 }
 
-// FAST, with the dimension's three scaled uniforms drawn earlier (in the same
-// order): a = w*r1, b = c1*r2, c = c2*r3.
-__device__ __forceinline__ void pso_update_drawn(float& x, float& v, float pb, float g, float a, float b, float c)
-{
-    v = __builtin_fmaf(a, v, __builtin_fmaf(b, pb - x, c * (g - x)));
-    x += v;
-}
-
 // clamp (src/matrix_operations.cuh:187-190)
 __device__ __forceinline__ float clamp_ref(float v, float lo, float hi) { return fminf(fmaxf(v, lo), hi); }
 
@@ -1081,9 +1009,7 @@ __device__ __forceinline__ float clamp_ref(float v, float lo, float hi) { return
 template <int MODE>
 __device__ __forceinline__ float clamp_mode(float v, float lo, float hi)
 {
-#if IKPSO_CLAMP_MED3
     if constexpr (MODE == IKPSO_ARITH_FAST) return __builtin_amdgcn_fmed3f(v, lo, hi);
-#endif
     return clamp_ref(v, lo, hi);
 }
 

@@ -57,6 +57,9 @@ struct ChainHost {
     uint64_t free_mask = 0;
     int dfree = 0;
     bool masked = false;          // some Euler angle is locked: runtime-term kernels only
+    // a free angle's clamp bound or rest value lies beyond kHwTrigMaxAbs: FAST
+    // solves take the polynomial sin/cos (the collider builds, with no collider)
+    bool poly_trig = false;
     size_t dh_off = 0;            // TopoDH constants in aux (ChainConsts::dh_off), 12 J + 4 floats
     int dof() const { return dfree; }
     int kernel_dims() const { return topo == TopoKind::DH ? J : 3 * J; }
@@ -91,20 +94,9 @@ __host__ __device__ constexpr int kCoopThreads()
     return D <= 30 ? 1024 : 512;
 }
 
-// Experiment (off): for long chains (D > 30: 512-lane chunks, x and v take 120
-// VGPRs at D = 60) keep each chunk's local bests in a global plane (L2-resident:
-// 120 KiB per CU) and the velocities in LDS, so only the positions occupy VGPRs.
-// Measured on config 5 (2048 swarms x 4096 x 100): no spills in the iteration
-// loop and 3958 issue slots per update instead of 4651, yet 119-122 ms against
-// 97.6 ms -- the LDS velocity round trip and the global loads cost more than the
-// registers they free at 2 waves per SIMD.
 #ifndef IKPSO_COOP_TIMING
 #define IKPSO_COOP_TIMING 0  // measurement builds: per-workgroup cycles in the step and in the hand-off
 #endif
-#ifndef IKPSO_COOP_PBG
-#define IKPSO_COOP_PBG 0
-#endif
-__host__ __device__ constexpr bool coop_global_pbest(int D) { return IKPSO_COOP_PBG && D > 30; }
 
 // Published record of one chunk, in 8-byte granules {value, tag}: the key, then
 // the D floats of the chunk winner's local best; padded to a 128-B multiple.
@@ -115,10 +107,13 @@ __host__ __device__ constexpr int kCoopSlot(int D) { return ((D + 1 + 15) / 16) 
 constexpr uint32_t kCoopSpinLimit = 1u << 22;
 // Latency variant of the cooperative kernel (few swarms): 256-lane chunks,
 // one wave per SIMD, a swarm of 1024 over 4 CUs.
-#ifndef IKPSO_COOP_LATENCY_THREADS
-#define IKPSO_COOP_LATENCY_THREADS 256
-#endif
-constexpr int kCoopLatencyThreads = IKPSO_COOP_LATENCY_THREADS;
+constexpr int kCoopLatencyThreads = 256;
+// Largest |angle| the FAST kernels hand to the transcendental unit's v_sin/v_cos
+// (which take x / 2pi): tools/probes/trig_probe.hip measures the max abs error
+// at 4.8e-7 on [0, 2pi] and 7.0e-6 on [-100, 100] (the fp32 rounding of x / 2pi
+// grows with |x|).  Chains whose clamp bounds or rest angles reach beyond it
+// solve with the 1-ulp polynomial instead (ChainHost::poly_trig).
+constexpr float kHwTrigMaxAbs = 100.0f;
 template <int J>
 ChainConsts<J> make_consts(const ChainHost& h)
 {

@@ -72,7 +72,6 @@ struct SwarmIO {
     int32_t coop_ng;
     int32_t coop_block;       // workgroup size (kCoopThreads<J>() or kCoopLatencyThreads)
     uint32_t coop_spin_limit; // polls before a group wait gives up (0: give up at the first unmet poll)
-    float* coop_pbest;        // [NG*G][D][BLOCK] local-best planes of the long-chain build (coop_global_pbest)
     unsigned long long* coop_timing;  // IKPSO_COOP_TIMING builds: [NG*G][4] cycle counts (else null)
 };
 

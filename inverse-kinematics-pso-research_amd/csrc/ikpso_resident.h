@@ -19,41 +19,18 @@
 #include "ikpso_kernels.h"
 #include "ikpso_swarm.h"
 
-#ifndef IKPSO_DH_NODE_BARRIER
-#define IKPSO_DH_NODE_BARRIER 0
-#endif
-// Software-pipelined FAST iteration (swarm_step_ahead) for chains of up to this
-// many dimensions: the 4-wave kernels (config 3: -4 % kernel time).  The 2-wave
-// D = 60 kernel spills the extra live node under it (3x slower), so not there.
-#ifndef IKPSO_NODE_BARRIER_EVERY
-#define IKPSO_NODE_BARRIER_EVERY 1  // long-chain step: scheduling region = this many nodes
-#endif
-#ifndef IKPSO_DRAWS_AHEAD
-#define IKPSO_DRAWS_AHEAD 0
-#endif
-#ifndef IKPSO_TRIG_AHEAD_MAX_D
-#define IKPSO_TRIG_AHEAD_MAX_D 30
-#endif
-#ifndef IKPSO_PRIO_LEVEL
-// progress-levelled wave priority inside the iteration: 0 = off, 1 = the
-// long-chain (2-wave) step over 4 levels and the pipelined 4-wave step over 2,
-// 2 = the 4-wave tip-backward step too.  Measured: config 5 81.1 -> 77.4 ms on
-// 2048 swarms x 100 iterations (profiles/r02c, r02d variant_timings); config 3
-// 48.3 -> 47.3 ms with 2 levels, 51.7 ms with 4 (profiles/r02g); the folded DH
-// arm's 4-wave tip-backward step unchanged within noise (so left off)
-#define IKPSO_PRIO_LEVEL 1
-#endif
-#ifndef IKPSO_TIP_BACKWARD_SHORT
-#define IKPSO_TIP_BACKWARD_SHORT 1  // the tip-backward step in the 4-wave (D <= 30) kernels too
-#endif
-#ifndef IKPSO_PRIO_LEVELS
-#define IKPSO_PRIO_LEVELS 4  // levels of the 2-wave steps
-#endif
-#ifndef IKPSO_PRIO_LEVELS_4WAVE
-#define IKPSO_PRIO_LEVELS_4WAVE 2  // levels of the pipelined 4-wave step
-#endif
-
 namespace ikpso {
+
+// Chains of up to this many dimensions run 4 waves per SIMD (1024-lane
+// workgroups) and take the software-pipelined FAST step (swarm_step_ahead);
+// longer ones run 2 waves per SIMD, where the extra live node spills (3x slower).
+constexpr int kTrigAheadMaxD = 30;
+// Progress-levelled wave priority (progress_prio): levels of the 2-wave steps
+// and of the pipelined 4-wave step.  Measured: config 5 81.1 -> 77.4 ms on 2048
+// swarms x 100 iterations with 4 levels (profiles/r02c, r02d variant_timings);
+// config 3 48.3 -> 47.3 ms with 2 levels, 51.7 ms with 4 (profiles/r02g); the
+// folded DH arm's 4-wave tip-backward step unchanged within noise (so none).
+constexpr int kPrioLevels2Wave = 4, kPrioLevels4Wave = 2;
 
 // Progress-levelled wave priority: entering node k of J a wave sets its issue
 // priority to (L-1) - L(k-1)/J, so a wave that has run ahead of the others on
@@ -63,11 +40,11 @@ namespace ikpso {
 // one runs its tail alone, with nothing to hide its dependency latency.
 // With 4 waves per SIMD, 2 levels (4 keep them in lockstep, contending for the
 // same unit at the same time).
-template <int J, int LEVEL = 1, int L = IKPSO_PRIO_LEVELS>
+template <int J, int L>
 __device__ __forceinline__ void progress_prio(int k)
 {
-    static_assert(L >= 2 && L <= 4, "priority levels 2..4");
-    if constexpr (IKPSO_PRIO_LEVEL >= LEVEL) {
+    static_assert(L == 0 || (L >= 2 && L <= 4), "priority levels: none or 2..4");
+    if constexpr (L > 0) {
         switch ((L - 1) - (L * (k - 1)) / J) {
         case 3: __builtin_amdgcn_s_setprio(3); break;
         case 2: __builtin_amdgcn_s_setprio(2); break;
@@ -119,12 +96,12 @@ __device__ __forceinline__ float swarm_step_ahead(const ChainConsts<Topo::J>& cc
     constexpr int J = Topo::J, A = Topo::A;
     constexpr bool HW = kHwTrig<Topo, MODE, TERMS>;
     FitnessFor<Topo, MODE, TERMS> acc(cc, sh.dh, sh.soft);
-    progress_prio<J, 1, IKPSO_PRIO_LEVELS_4WAVE>(1);
+    progress_prio<J, kPrioLevels4Wave>(1);
     update_node<Topo, MODE, TERMS, BLOCK>(cc, sh, s_pb, tid, 1, x, v, coef, rng);
     NodeTrig<A> cur = node_trig<HW, A>(x);
 #pragma unroll
     for (int k = 1; k <= J; ++k) {
-        if (k > 1) progress_prio<J, 1, IKPSO_PRIO_LEVELS_4WAVE>(k);
+        if (k > 1) progress_prio<J, kPrioLevels4Wave>(k);
         NodeTrig<A> nxt = cur;
         if (k < J) {
             update_node<Topo, MODE, TERMS, BLOCK>(cc, sh, s_pb, tid, k + 1, x, v, coef, rng);
@@ -137,9 +114,7 @@ __device__ __forceinline__ float swarm_step_ahead(const ChainConsts<Topo::J>& cc
         for (int c = 0; c < 3; ++c) tgt[c] = Topo::effector(k) ? sh.tgt[3 * (k - 1) + c] : 0.0f;
         acc.node_trig(cc, k, x + A * (k - 1), cur, rest, tgt, nullptr);
         cur = nxt;
-#if !IKPSO_RES_NO_NODE_BARRIER
-        if (!Topo::kDH || IKPSO_DH_NODE_BARRIER) __builtin_amdgcn_sched_barrier(0);
-#endif
+        if (!Topo::kDH) __builtin_amdgcn_sched_barrier(0);
     }
     return acc.finish(cc);
 }
@@ -155,7 +130,7 @@ __device__ __forceinline__ void swarm_step_tip(const ChainConsts<Topo::J>& cc, S
                                                const PsoCoef& coef, Rng& rng)
 {
     constexpr int J = Topo::J, A = Topo::A, D = Topo::D;
-    constexpr int PL = D > IKPSO_TRIG_AHEAD_MAX_D ? 1 : 2;  // wave priority: the 2-wave kernels
+    constexpr int PL = D > kTrigAheadMaxD ? kPrioLevels2Wave : 0;  // wave priority: the 2-wave kernels
     using Acc = TipAccFor<Topo, MODE, TERMS>;
     Acc acc(sh.dh, sh.soft);
     float npb[A], ng[A], nrest[A];
@@ -228,11 +203,11 @@ __device__ __forceinline__ void swarm_step(const ChainConsts<Topo::J>& cc, Swarm
 {
     constexpr int J = Topo::J, A = Topo::A, D = Topo::D;
     constexpr bool MASK = kMasked<Topo, TERMS>;
-    if constexpr (kTipBackward<Topo, MODE, TERMS> && (Topo::D > IKPSO_TRIG_AHEAD_MAX_D || IKPSO_TIP_BACKWARD_SHORT)) {
+    if constexpr (kTipBackward<Topo, MODE, TERMS>) {
         swarm_step_tip<Topo, MODE, TERMS, BLOCK>(cc, sh, s_pb, tid, x, v, pbf, coef, rng);
         return;
     }
-    if constexpr (MODE == IKPSO_ARITH_FAST && Topo::D <= IKPSO_TRIG_AHEAD_MAX_D) {
+    if constexpr (MODE == IKPSO_ARITH_FAST && Topo::D <= kTrigAheadMaxD) {
         // updateLocalBests (src/kernel.cu:202-221): strict improvement
         const float f = swarm_step_ahead<Topo, MODE, TERMS, BLOCK>(cc, sh, s_pb, tid, x, v, coef, rng);
         if (f < pbf) {
@@ -243,19 +218,6 @@ __device__ __forceinline__ void swarm_step(const ChainConsts<Topo::J>& cc, Swarm
         return;
     }
     FitnessFor<Topo, MODE, TERMS> acc(cc, sh.dh, sh.soft);
-    // FAST long chains: node k+1's draws are generated while node k is folded
-    // into the FK (integer work the scheduler can interleave with the float
-    // chain; the draw order is unchanged)
-    constexpr bool AHEAD = IKPSO_DRAWS_AHEAD && MODE == IKPSO_ARITH_FAST && !MASK;
-    float nd[A][3];
-    if constexpr (AHEAD) {
-#pragma unroll
-        for (int ax = 0; ax < A; ++ax) {
-            nd[ax][0] = rng.scaled(coef.wq, coef.wh);
-            nd[ax][1] = rng.scaled(coef.c1q, coef.c1h);
-            nd[ax][2] = rng.scaled(coef.c2q, coef.c2h);
-        }
-    }
     float npb[A], ng[A], nrest[A], ntgt[3];
 #pragma unroll
     for (int ax = 0; ax < A; ++ax) {
@@ -267,7 +229,7 @@ __device__ __forceinline__ void swarm_step(const ChainConsts<Topo::J>& cc, Swarm
     for (int c = 0; c < 3; ++c) ntgt[c] = Topo::effector(1) ? sh.tgt[c] : 0.0f;
 #pragma unroll
     for (int k = 1; k <= J; ++k) {
-        progress_prio<J, (D > IKPSO_TRIG_AHEAD_MAX_D ? 1 : 2)>(k);  // the 2-wave kernels
+        progress_prio<J, (D > kTrigAheadMaxD ? kPrioLevels2Wave : 0)>(k);  // the 2-wave kernels
         float cpb[A], cg[A], crest[A], ctgt[3];
 #pragma unroll
         for (int ax = 0; ax < A; ++ax) {
@@ -292,30 +254,14 @@ __device__ __forceinline__ void swarm_step(const ChainConsts<Topo::J>& cc, Swarm
         for (int ax = 0; ax < A; ++ax) {
             const int d = A * (k - 1) + ax;
             if (MASK && !dim_free(cc, d)) continue;  // locked: stays at rest
-            if constexpr (AHEAD)
-                pso_update_drawn(x[d], v[d], cpb[ax], cg[ax], nd[ax][0], nd[ax][1], nd[ax][2]);
-            else
-                pso_update<MODE>(x[d], v[d], cpb[ax], cg[ax], coef, rng);
+            pso_update<MODE>(x[d], v[d], cpb[ax], cg[ax], coef, rng);
             if constexpr (TERMS & kTermUniformBounds)
                 x[d] = clamp_mode<MODE>(x[d], cc.lo[0], cc.hi[0]);
             else
                 x[d] = clamp_mode<MODE>(x[d], sh.lo[d], sh.hi[d]);
         }
-        if constexpr (AHEAD) {
-            if (k < J) {
-#pragma unroll
-                for (int ax = 0; ax < A; ++ax) {
-                    nd[ax][0] = rng.scaled(coef.wq, coef.wh);
-                    nd[ax][1] = rng.scaled(coef.c1q, coef.c1h);
-                    nd[ax][2] = rng.scaled(coef.c2q, coef.c2h);
-                }
-            }
-        }
         acc.node(cc, k, x + A * (k - 1), crest, ctgt, nullptr);
-#if !IKPSO_RES_NO_NODE_BARRIER
-        if ((!Topo::kDH || IKPSO_DH_NODE_BARRIER) && (k % IKPSO_NODE_BARRIER_EVERY == 0 || k == J))
-            __builtin_amdgcn_sched_barrier(0);
-#endif
+        if (!Topo::kDH) __builtin_amdgcn_sched_barrier(0);
     }
 
     // updateLocalBests (src/kernel.cu:202-221): strict improvement
@@ -385,12 +331,7 @@ __device__ __forceinline__ void swarm_resident_body(const ChainConsts<Topo::J>& 
         swarm_step<Topo, MODE, TERMS, BLOCK>(cc, sh, s_pb, tid, x, v, pbf, coef, rng);
 
         // thrust::min_element + `globalMin > currentGlobalMin` (src/kernel.cu:315-323)
-#if IKPSO_ABL_NOSYNC  // timing-only ablation: no swarm argmin
-        const uint32_t bmin = gkey;
-        asm volatile("" ::"v"(pbf));
-#else
         const uint32_t bmin = swarm_argmin(sh, (it + 1) & 1, active ? ordered_key(pbf) : 0xFFFFFFFFu, &bidx);
-#endif
         if (bmin < gkey) {  // uniform across the workgroup
             gkey = bmin;
             copy_gbest<Topo, BLOCK>(sh, s_pb, bidx);

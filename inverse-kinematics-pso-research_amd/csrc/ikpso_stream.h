@@ -19,14 +19,10 @@
 #include "ikpso_kernels.h"
 #include "ikpso_swarm.h"
 
-#ifndef IKPSO_STREAM_AHEAD
-#define IKPSO_STREAM_AHEAD 2
-#endif
-#ifndef IKPSO_STREAM_PBEST
-#define IKPSO_STREAM_PBEST 1
-#endif
-
 namespace ikpso {
+
+// Nodes of x / v / local best loaded ahead of their use in k_stream_step.
+constexpr int kStreamAhead = 2;
 
 // Resolve the swarm's global best as of the end of launch t-1: reduce the C
 // chunk partials of slot (t-1)&1, compare with the global best of slot
@@ -167,13 +163,21 @@ __global__ void __launch_bounds__(kStreamChunk) k_stream_step(const ChainConsts<
         // update-all-then-evaluate with the same values and accumulation order,
         // while only a handful of angles are live at a time.
         const PsoCoef coef = pso_coef(cc);
+        // kTipBackward builds (serial chains with only the tip's position in the
+        // fitness, and the folded chain): every node updated first, then the tip
+        // evaluated from the tip back -- the form the resident and cooperative
+        // kernels use (swarm_step_tip), so a streaming solve (or a cooperative
+        // solve's fallback) rounds like them
+        constexpr bool TIP = kTipBackward<Topo, MODE, TERMS>;
         FitnessFor<Topo, MODE, TERMS> acc(cc, sh.dh, sh.soft);
+        TipAccFor<Topo, MODE, TERMS> tb(sh.dh, sh.soft);
+        float xs[TIP ? D : 1];
         // Loads are software-pipelined AHEAD nodes ahead (a ring of AHEAD+1
         // node slots in registers, indices resolved at compile time) and every
         // node ends in a scheduling barrier: left alone, the compiler hoists
         // all 9J loads to the top (256 VGPRs, one wave per SIMD,
         // latency-bound); one node ahead leaves HBM latency exposed.
-        constexpr int AHEAD = (IKPSO_STREAM_AHEAD < J) ? IKPSO_STREAM_AHEAD : J;
+        constexpr int AHEAD = (kStreamAhead < J) ? kStreamAhead : J;
         float ring[AHEAD + 1][3 * A];
 #pragma unroll
         for (int s = 0; s < AHEAD; ++s)
@@ -214,19 +218,24 @@ __global__ void __launch_bounds__(kStreamChunk) k_stream_step(const ChainConsts<
                     cx[ax] = clamp_mode<MODE>(cx[ax], sh.lo[d], sh.hi[d]);
                 pl.st(0, d, cx[ax]);
             }
-            acc.node(cc, kn, cx, sh.rest + A * (kn - 1), sh.tgt + 3 * (kn - 1), nullptr);
+            if constexpr (TIP) {
+#pragma unroll
+                for (int ax = 0; ax < A; ++ax) xs[A * (kn - 1) + ax] = cx[ax];
+                tb.angles(kn, cx, sh.rest + A * (kn - 1));
+            } else {
+                acc.node(cc, kn, cx, sh.rest + A * (kn - 1), sh.tgt + 3 * (kn - 1), nullptr);
+            }
             __builtin_amdgcn_sched_barrier(0);
         }
-        // updateLocalBests (src/kernel.cu:202-221)
-        const float f = acc.finish(cc);
-#if IKPSO_STREAM_PBEST == 0
-        if (f < pbf) {
-            pbf = f;
-            io.pbf[b * P + i] = f;
+        float f;
+        if constexpr (TIP) {
 #pragma unroll
-            for (int d = 0; d < D; ++d) pl.st(2, d, pl.ld(0, d));  // this lane's own stores
+            for (int kn = J; kn >= 1; --kn) tb.back(cc, kn, node_trig<decltype(tb)::HW, A>(xs + A * (kn - 1)));
+            f = tb.finish(cc, sh.tgt + 3 * (J - 1));
+        } else {
+            f = acc.finish(cc);
         }
-#else
+        // updateLocalBests (src/kernel.cu:202-221)
         // Whole-line stores only: a store covering part of a 128-B line makes
         // the memory side fetch the line first.  A wave with no improving lane
         // writes nothing; otherwise every lane rewrites its local best (its new
@@ -242,7 +251,6 @@ __global__ void __launch_bounds__(kStreamChunk) k_stream_step(const ChainConsts<
                 pl.st(2, d, imp ? xn : po);
             }
         }
-#endif
         io.rng[0 * n + k] = rng.d;
         io.rng[1 * n + k] = rng.v0;
         io.rng[2 * n + k] = rng.v1;

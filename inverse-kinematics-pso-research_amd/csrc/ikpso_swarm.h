@@ -182,7 +182,7 @@ __device__ __forceinline__ void copy_gbest(SwarmShared<Topo>& sh, const float* s
 inline int term_set(const ChainHost& ch)
 {
     return (ch.use_posref ? kTermPosRef : 0) | (ch.use_penalty ? kTermPenalty : 0) |
-           (ch.uniform_bounds ? kTermUniformBounds : 0) | (ch.num_coll > 0 ? kTermColliders : 0) |
+           (ch.uniform_bounds ? kTermUniformBounds : 0) | (ch.num_coll > 0 || ch.poly_trig ? kTermColliders : 0) |
            (ch.masked ? kTermMask : 0);
 }
 
@@ -215,8 +215,11 @@ inline hipError_t with_runtime_terms(const ChainHost& ch, F&& f)
     if constexpr (Topo::kDH) {  // every term set of a folded chain has its own build (dh_terms)
         return hipErrorNotSupported;
     } else {
-        if (ch.num_coll > 0 && ch.masked) return f(std::integral_constant<int, kTermRuntime | kTermColliders | kTermMask>{});
-        if (ch.num_coll > 0) return f(std::integral_constant<int, kTermRuntime | kTermColliders>{});
+        // the collider builds also carry chains with wide angle ranges (poly_trig:
+        // polynomial sin/cos; an empty collider loop)
+        const bool coll = ch.num_coll > 0 || ch.poly_trig;
+        if (coll && ch.masked) return f(std::integral_constant<int, kTermRuntime | kTermColliders | kTermMask>{});
+        if (coll) return f(std::integral_constant<int, kTermRuntime | kTermColliders>{});
         if (ch.masked) return f(std::integral_constant<int, kTermRuntime | kTermMask>{});
         return f(std::integral_constant<int, kTermRuntime>{});
     }

@@ -6,7 +6,7 @@ reference's solver interface (initGenerators / calculatePSO) plus the batched
 multi-swarm API and the scene model on the caller's side of the boundary.
 """
 from ._abi import (ARITH_FAST, ARITH_REFERENCE, COLLIDER_DTYPE, NODE, NODE_DTYPE, NODE_EFFECTOR, NODE_ORIGIN,
-                   RNG_DTYPE, IkpsoError, load)
+                   RNG_DTYPE, IkpsoError, StaleLibraryError, build_id, load)
 from .scene import (RESET_TARGETS, EffectorNode, Node, OriginNode, Scene, TargetNode, check_distance,
                     init_colliders, reference_scene, serial_chain)
 from .solver import (MAIN_FITNESS, MAIN_PSO, BatchSolver, FitnessConfig, PSOConfig, calculate_pso,
@@ -16,7 +16,7 @@ from .workloads import Workload, workload
 
 __all__ = [
     "ARITH_FAST", "ARITH_REFERENCE", "COLLIDER_DTYPE", "init_colliders", "make_collider", "NODE", "NODE_DTYPE", "NODE_EFFECTOR", "NODE_ORIGIN", "RNG_DTYPE",
-    "IkpsoError", "load", "RESET_TARGETS", "EffectorNode", "Node", "OriginNode", "Scene", "TargetNode",
+    "IkpsoError", "StaleLibraryError", "build_id", "load", "RESET_TARGETS", "EffectorNode", "Node", "OriginNode", "Scene", "TargetNode",
     "check_distance", "reference_scene", "serial_chain", "MAIN_FITNESS", "MAIN_PSO", "BatchSolver",
     "FitnessConfig", "PSOConfig", "calculate_pso", "init_generators", "init_generators_seeded",
     "particles_tensor", "rng_tensor", "Workload", "workload", "DHArm", "dh_arm", "dh_forward",

@@ -72,7 +72,7 @@ COLLIDER_DTYPE = np.dtype(
 )
 assert COLLIDER_DTYPE.itemsize == 48
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 FLAG_POSREF_NODE_SLOT = 1  # IKPSO_FLAG_POSREF_NODE_SLOT
 FLAG_NO_FOLD = 2  # IKPSO_FLAG_NO_FOLD
@@ -141,12 +141,14 @@ SIGNATURES = {
     "ikpso_solver_fallbacks": (_i64, [_vp]),
     "ikpso_coop_fallbacks": (_i64, []),
     "ikpso_solver_evaluate": (_i32, [_vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp]),
+    "ikpso_solver_generator_states": (_i32, [_vp, _i64, _i64, _vp, _vp]),
     "ikpso_solver_dof": (ctypes.c_int, [_vp]),
     "ikpso_solver_effectors": (ctypes.c_int, [_vp]),
     "ikpso_solver_kernel_name": (ctypes.c_char_p, [_vp]),
     "ikpso_abi_version": (ctypes.c_int, []),
     "ikpso_status_string": (ctypes.c_char_p, [_i32]),
     "ikpso_last_hip_error": (ctypes.c_int, []),
+    "ikpso_build_id": (ctypes.c_char_p, []),
 }
 
 _LIB = None
@@ -161,8 +163,20 @@ class IkpsoError(RuntimeError):
         self.status = status
 
 
+class StaleLibraryError(RuntimeError):
+    """libikpso.so was built from other sources than the tree it is loaded from."""
+
+
+def build_id() -> str:
+    """The loaded library's source hash (``ikpso_build_id``)."""
+    return load().ikpso_build_id().decode()
+
+
 def load() -> ctypes.CDLL:
-    """Load libikpso.so (RTLD_GLOBAL not needed).  Raises if it is missing."""
+    """Load libikpso.so (RTLD_GLOBAL not needed).  Raises if it is missing, has
+    another ABI version, or was built from other sources than this tree
+    (``ikpso_build_id`` vs ``_buildid.tree_id()``; IKPSO_ALLOW_STALE=1 accepts
+    it, for variant builds loaded through IKPSO_LIB)."""
     global _LIB
     if _LIB is not None:
         return _LIB
@@ -179,6 +193,13 @@ def load() -> ctypes.CDLL:
         fn.argtypes = args
     if lib.ikpso_abi_version() != ABI_VERSION:
         raise RuntimeError(f"{path}: ABI version {lib.ikpso_abi_version()}, expected {ABI_VERSION} (rebuild)")
+    from . import _buildid
+
+    built, tree = lib.ikpso_build_id().decode(), _buildid.tree_id()
+    if tree is not None and built != tree and os.environ.get("IKPSO_ALLOW_STALE") != "1":
+        raise StaleLibraryError(
+            f"{path} was built from sources {built}, this tree is {tree}: rebuild (make -C "
+            "inverse-kinematics-pso-research_amd/csrc), or set IKPSO_ALLOW_STALE=1 for a variant build")
     _LIB = lib
     return lib
 

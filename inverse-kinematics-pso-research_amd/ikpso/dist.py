@@ -31,12 +31,14 @@ def pack_results(angles, fitness, residual):
     return torch.cat(cols, dim=1).contiguous()
 
 
-def gather_rows(local, total: int, world: int, group=None):
-    """All-gather per-rank row blocks (possibly uneven) into [total, cols] on every rank."""
+def gather_rows(local, total: int, world: int, group=None, force: bool = False):
+    """All-gather per-rank row blocks (possibly uneven) into [total, cols] on every rank.
+    With one rank the rows are returned as they are, unless `force` (tests: drive
+    the collective through a world-1 process group)."""
     import torch
     import torch.distributed as dist
 
-    if world == 1:
+    if world == 1 and not force:
         return local
     cols = local.shape[1]
     counts = [shard_range(total, world, r)[1] for r in range(world)]

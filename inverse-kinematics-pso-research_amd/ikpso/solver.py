@@ -283,6 +283,16 @@ class BatchSolver:
         """Cooperative solves of this solver that were re-run on the streaming kernels."""
         return int(self._lib.ikpso_solver_fallbacks(self._h))
 
+    def generator_states(self, first_swarm: int = 0, count: Optional[int] = None, stream=None) -> np.ndarray:
+        """The solver-owned generator states of local swarms [first_swarm, first_swarm + count):
+        int32 words [count * P, 12] (curandState layout, swarm-major), after settling a
+        pending solve (ikpso_solver_generator_states)."""
+        n = (self.capacity - int(first_swarm)) if count is None else int(count)
+        out = np.zeros((n * self.P, RNG_WORDS), dtype=np.int32)
+        _abi.check(self._lib.ikpso_solver_generator_states(self._h, int(first_swarm), n, out.ctypes.data,
+                                                           _stream_handle(stream)), "ikpso_solver_generator_states")
+        return out
+
     def evaluate(self, angles, targets=None, rest=None, stream=None):
         """Device FK + fitness for angle vectors [n, D]: (fitness [n], node positions [n, J, 3])."""
         torch = _torch()

@@ -382,7 +382,7 @@ static float fitness_soa(const orc_node* chain, int node_count, const float* pos
 {
     int fd[3 * 64];
     const int D = free_dims(pen, node_count, fd);
-    float x[3 * 64], ang[3 * 64];
+    float x[3 * 64], ang[3 * 64] = {0};  /* expand_angles fills ang[0 .. 3J) */
     for (int d = 0; d < D; d++) x[d] = particles[pidx(count, i, 0, d, D)];
     expand_angles(chain, node_count, pen, x, ang);
     return fitness_pen(chain, node_count, positions, ang, aw, dw, pen);

@@ -44,7 +44,7 @@ def test_compat_symbols_exported():
 
 def test_abi_version_and_strings():
     lib = _abi.load()
-    assert lib.ikpso_abi_version() == 4
+    assert lib.ikpso_abi_version() == 5
     assert lib.ikpso_status_string(0) == b"ok"
     assert lib.ikpso_status_string(2) == b"unsupported configuration"
 
@@ -92,6 +92,7 @@ def test_validation_without_device_work():
     assert lib.ikpso_init_generators_seeded(None, 5, 0, None) == _abi.IKPSO_ERR_INVALID_ARG
     assert lib.ikpso_solver_seed(None, 1, 0, 0, None) == _abi.IKPSO_ERR_INVALID_ARG
     assert lib.ikpso_solve_batch(None, None, None, 1, 1, None, None, None, None) == _abi.IKPSO_ERR_INVALID_ARG
+    assert lib.ikpso_solver_generator_states(None, 0, 1, None, None) == _abi.IKPSO_ERR_INVALID_ARG
     # a collider count without colliders is refused before any device work
     pso = _abi.PSOConfig(0.5, 0.5, 1.25, 15)
     fit = _abi.FitnessConfig(3.0, 0.0, 0.1)
@@ -101,6 +102,31 @@ def test_validation_without_device_work():
         _abi.IKPSO_ERR_INVALID_ARG
     assert lib.ikpso_calculate_pso(None, None, None, None, 0, None, 8, pso, fit, None, None, 0, None) == \
         _abi.IKPSO_ERR_INVALID_ARG
+
+
+def test_build_id_is_the_tree_hash():
+    """The library carries the hash of the sources it was built from (make writes it)."""
+    from ikpso import _buildid
+
+    lib = _abi.load()
+    assert lib.ikpso_build_id().decode() == _buildid.tree_id()
+    assert len(_buildid.tree_id()) == 16
+    assert _buildid.build_id("-DX=1").startswith(_buildid.tree_id() + "+")
+
+
+def test_stale_library_is_refused(monkeypatch):
+    """A library built from other sources (e.g. a failed rebuild left the old one
+    in place) is refused at load; IKPSO_ALLOW_STALE=1 accepts it (variant builds)."""
+    from ikpso import _buildid
+
+    monkeypatch.setattr(_abi, "_LIB", None)
+    monkeypatch.setattr(_buildid, "tree_id", lambda: "0123456789abcdef")
+    monkeypatch.delenv("IKPSO_ALLOW_STALE", raising=False)
+    with pytest.raises(_abi.StaleLibraryError, match="0123456789abcdef"):
+        _abi.load()
+    monkeypatch.setattr(_abi, "_LIB", None)
+    monkeypatch.setenv("IKPSO_ALLOW_STALE", "1")
+    assert _abi.load().ikpso_abi_version() == _abi.ABI_VERSION
 
 
 def test_product_has_no_cpu_fallback():

@@ -498,3 +498,28 @@ def test_frames_to_converge_matches_frames3(device, golden, tmp_path):
     assert len(lines["IK-diagnostics-degrees.txt"]) == sum(frames)
     assert all(l.count(";") == 21 for l in lines["IK-diagnostics-positions.txt"])
     print("frames to converge:", frames, "median", np.median(frames), "mean", np.mean(frames))
+
+
+def test_wide_angle_ranges_take_the_polynomial(oracle, device):
+    """FAST solves hand angles to the transcendental unit's v_sin/v_cos only while
+    every clamp bound and rest angle lies within kHwTrigMaxAbs = 100 rad (its
+    error grows with |x|: tools/probes/trig_probe.hip); a chain reaching beyond
+    takes the 1-ulp polynomial.  Here the joints start near 800 rad (start pose)
+    inside +-1000 rad bounds, and the solve stays within tier A of the oracle
+    (angles of ~800 rad carry a 6e-5 ulp, hence the angle tolerance)."""
+    wl = ikpso.workload(3)
+    chain = wl.chain.copy()
+    chain["min_rotation"][1:] = -1000.0
+    chain["max_rotation"][1:] = 1000.0
+    B, P, I = 4, 1024, 20
+    tg = wl.targets(0, B)
+    sp = (800.0 + np.random.default_rng(7).uniform(0.0, 2.0, (B, 21))).astype(np.float32)
+    s = ikpso.BatchSolver(chain, P, pso=wl.pso)
+    s.seed(B)
+    ang, fit, res = (t.cpu().numpy() for t in s.solve(dev(tg), dev(sp), iterations=I))
+    s.close()
+    ostate = oracle.init_generators(B * P, 0)
+    oang, ofit, ores = oracle.solve_batch(chain, tg, sp, P, I, ostate, threads=4)
+    assert np.max(np.abs(ang - oang)) < 1e-3, np.max(np.abs(ang - oang))  # ~16 ulp at 800 rad
+    assert np.max(np.abs(fit - ofit) / ofit) < 1e-4, np.max(np.abs(fit - ofit) / ofit)
+    assert np.max(np.abs(res - ores)) < 1e-3

@@ -14,6 +14,10 @@ run() {  # run PASS ROCPROF_ARGS...
     > "gpurun_out/${NAME}_$pass.log" 2>&1
   local rc=$?; echo "   rc=$rc"; [ $rc -eq 0 ] || { tail -20 "gpurun_out/${NAME}_$pass.log"; exit $rc; }
 }
+# the library build the counters are measured on (bench.py marks a roofline whose counters came from
+# another build as stale)
+python3 -c "import sys; sys.path.insert(0, 'inverse-kinematics-pso-research_amd'); import ikpso; print(ikpso.build_id())" \
+  > "gpurun_out/${NAME}_build_id.txt" || exit 9
 run trace --kernel-trace --stats
 run valu --pmc SQ_INSTS_VALU SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVES GRBM_GUI_ACTIVE
 run fetch --pmc FETCH_SIZE

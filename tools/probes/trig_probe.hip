@@ -113,7 +113,10 @@ int main()
 {
     const char* names[NV] = {"sincos_fast (current FAST)", "__sinf/__cosf", "sincos_v2 (bitop3 signs)",
                              "sincos_v3 (2-fma reduction)", "v_sin/v_cos(x/2pi)", "v_sin/v_cos(fract(x/2pi))"};
-    const float ranges[4][2] = {{-7.0f, 7.0f}, {0.0f, 6.2831855f}, {-3.1415927f, 3.1415927f}, {-100.0f, 100.0f}};
+    // the last two: the FAST kernels' v_sin/v_cos range bound (kHwTrigMaxAbs, 100 rad) and the unit's own
+    // +-256 revolutions
+    const float ranges[6][2] = {{-7.0f, 7.0f},     {0.0f, 6.2831855f},   {-3.1415927f, 3.1415927f},
+                                {-100.0f, 100.0f}, {-400.0f, 400.0f}, {-1600.0f, 1600.0f}};
     Stats* st; unsigned* bb;
     hipMalloc(&st, sizeof(Stats)); hipMalloc(&bb, 8);
     for (auto& r : ranges) {

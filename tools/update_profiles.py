@@ -54,6 +54,9 @@ res = {
               f"{upd} particle-updates per dispatch; profiles/{rnd}/{name}_pmc_*.csv. lane-instr/update = "
               "SQ_INSTS_VALU * 64 / updates; bytes = (2*FETCH_SIZE + WRITE_SIZE) KiB*1024 / updates",
     "fetch_bytes": fb, "write_bytes": wb, "updates": upd,
+    # ikpso_build_id() of the library the counters were collected on (tools/gpu_profile.sh)
+    "build_id": (src / f"{name}_build_id.txt").read_text().strip() if (src / f"{name}_build_id.txt").exists()
+    else None,
 }
 if tu:
     import subprocess
