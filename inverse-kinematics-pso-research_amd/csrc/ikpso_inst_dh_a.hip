@@ -2,7 +2,7 @@
 #include "ikpso_topo_impl.h"
 
 namespace ikpso {
-#if IKPSO_WITH_OTHERS
+#if IKPSO_WITH_DH
 template struct ModeOps<TopoDH<3>, IKPSO_ARITH_FAST>;
 template struct ModeOps<TopoDH<4>, IKPSO_ARITH_FAST>;
 template struct ModeOps<TopoDH<5>, IKPSO_ARITH_FAST>;

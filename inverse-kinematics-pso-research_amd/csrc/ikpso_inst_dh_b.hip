@@ -2,7 +2,7 @@
 #include "ikpso_topo_impl.h"
 
 namespace ikpso {
-#if IKPSO_WITH_OTHERS
+#if IKPSO_WITH_DH
 template struct ModeOps<TopoDH<8>, IKPSO_ARITH_FAST>;
 template struct ModeOps<TopoDH<9>, IKPSO_ARITH_FAST>;
 template struct ModeOps<TopoDH<10>, IKPSO_ARITH_FAST>;

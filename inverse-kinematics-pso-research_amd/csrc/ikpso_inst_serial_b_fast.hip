@@ -3,7 +3,7 @@
 #include "ikpso_topo_impl.h"
 
 namespace ikpso {
-#if IKPSO_WITH_OTHERS
+#if IKPSO_WITH_DH
 template struct ModeOps<TopoSerialTip<9>, IKPSO_ARITH_FAST>;
 template struct ModeOps<TopoSerialTip<10>, IKPSO_ARITH_FAST>;
 template struct ModeOps<TopoSerialTip<11>, IKPSO_ARITH_FAST>;

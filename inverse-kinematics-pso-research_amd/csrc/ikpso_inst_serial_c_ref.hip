@@ -3,7 +3,7 @@
 #include "ikpso_topo_impl.h"
 
 namespace ikpso {
-#if IKPSO_WITH_OTHERS
+#if IKPSO_WITH_DH
 template struct ModeOps<TopoSerialTip<12>, IKPSO_ARITH_REFERENCE>;
 template struct ModeOps<TopoSerialTip<13>, IKPSO_ARITH_REFERENCE>;
 template struct ModeOps<TopoSerialTip<14>, IKPSO_ARITH_REFERENCE>;

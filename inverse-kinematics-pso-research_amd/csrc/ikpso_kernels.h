@@ -14,18 +14,27 @@
 #include "ikpso_params.h"
 
 // Experiment builds (tools/build_variants.sh) compile a subset of topologies.
+// DH_ONLY: the folded chains and the 6-14-joint serial chains they fold from.
 #if defined(IKPSO_EXPERIMENT_REF7_ONLY)
 #define IKPSO_WITH_REF7 1
 #define IKPSO_WITH_SERIAL20 0
 #define IKPSO_WITH_OTHERS 0
+#define IKPSO_WITH_DH 0
 #elif defined(IKPSO_EXPERIMENT_SERIAL20_ONLY)
 #define IKPSO_WITH_REF7 0
 #define IKPSO_WITH_SERIAL20 1
 #define IKPSO_WITH_OTHERS 0
+#define IKPSO_WITH_DH 0
+#elif defined(IKPSO_EXPERIMENT_DH_ONLY)
+#define IKPSO_WITH_REF7 0
+#define IKPSO_WITH_SERIAL20 0
+#define IKPSO_WITH_OTHERS 0
+#define IKPSO_WITH_DH 1
 #else
 #define IKPSO_WITH_REF7 1
 #define IKPSO_WITH_SERIAL20 1
 #define IKPSO_WITH_OTHERS 1
+#define IKPSO_WITH_DH 1
 #endif
 
 namespace ikpso {

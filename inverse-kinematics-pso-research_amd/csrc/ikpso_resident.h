@@ -366,8 +366,21 @@ __device__ __forceinline__ void swarm_resident_body(const ChainConsts<Topo::J>& 
 }
 
 
+// Waves per SIMD the resident kernel is compiled for.  The folded chain's
+// iteration is short (458 VALU instructions per wave-iteration at 7 free angles)
+// and two barriers of the swarm argmin end it: compiled for 8 waves per SIMD
+// (<= 64 VGPRs: x, v, the generator and a handful of FK temporaries; the
+// spills fall outside the iteration loop but for 0-11 scratch accesses per
+// iteration) two swarms share a CU and one's barrier waits hide under the
+// other's step -- iiwa arm, 4096 targets x 1024 x 500: 22.86 -> 18.43 ms
+// (9.17e10 -> 1.14e11 updates/s, profiles/r03a/variant_timings/var_dh7_waves.txt).
+// The Euler chains need more than 64 VGPRs (x, v and the node frames): one
+// 1024-lane workgroup per CU, 4 waves per SIMD.
+template <class Topo>
+constexpr int kResidentMinWaves = Topo::kDH ? 8 : 1;
+
 template <class Topo, int MODE, int TERMS>
-__global__ void __launch_bounds__(kResidentMaxThreads<Topo::D>())
+__global__ void __launch_bounds__(kResidentMaxThreads<Topo::D>(), kResidentMinWaves<Topo>)
     k_swarm_resident(const ChainConsts<Topo::J> cc, const SwarmIO io)
 {
     constexpr int NPB = Topo::D * kResidentMaxThreads<Topo::D>();

@@ -240,7 +240,7 @@ inline bool visit_topology(const ChainHost& ch, F&& f)
 #endif
     case TopoKind::SerialTip:
         switch (ch.J) {  // arm lengths of DH arms (6-14 nodes: 6-7 joints + d offsets) and BASELINE config 5
-#if IKPSO_WITH_OTHERS
+#if IKPSO_WITH_DH
 #define IKPSO_S(n) \
     case n: f(TopoSerialTip<n>{}); return true;
             IKPSO_S(6) IKPSO_S(7) IKPSO_S(8) IKPSO_S(9) IKPSO_S(10) IKPSO_S(11) IKPSO_S(12) IKPSO_S(13) IKPSO_S(14)
@@ -256,7 +256,7 @@ inline bool visit_topology(const ChainHost& ch, F&& f)
         break;
     case TopoKind::DH:
         switch (ch.J) {  // free angles of a folded serial chain (DH arms: 3-12)
-#if IKPSO_WITH_OTHERS
+#if IKPSO_WITH_DH
 #define IKPSO_D(n) \
     case n: f(TopoDH<n>{}); return true;
             IKPSO_D(3) IKPSO_D(4) IKPSO_D(5) IKPSO_D(6) IKPSO_D(7) IKPSO_D(8) IKPSO_D(9) IKPSO_D(10) IKPSO_D(11)

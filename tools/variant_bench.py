@@ -33,14 +33,14 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=500)
     ap.add_argument("--arith", default="fast")
-    ap.add_argument("--config", type=int, default=3, choices=[3, 5])
+    ap.add_argument("--config", default="3", choices=["3", "5", "dh7"])
     ap.add_argument("--particles", type=int, default=0, help="override the workload's swarm size")
     ap.add_argument("--kernel", type=int, default=0, help="ikpso_solver_desc.kernel (0 = AUTO)")
     a = ap.parse_args()
-    wl = ikpso.workload(a.config)
+    wl = ikpso.workload(int(a.config) if a.config.isdigit() else a.config)
     P, I, B = a.particles or wl.particles, a.iters, a.swarms
-    D = 3 * (wl.chain.shape[0] - 1)
-    tg = torch.from_numpy(wl.targets(0, B)).cuda()
+    D = wl.dof
+    tg = torch.from_numpy(np.ascontiguousarray(wl.targets(0, B))).cuda()
     outs = [torch.empty((B, D), device="cuda"), torch.empty(B, device="cuda"), torch.empty(B, device="cuda")]
     solvers = []
     for p in a.libs:
@@ -51,10 +51,15 @@ def main():
         desc.node_count = chain.shape[0]
         desc.particles = P
         desc.pso = _abi.PSOConfig(0.5, 0.5, 1.25, I)
-        desc.fit = _abi.FitnessConfig(3.0, 0.0, 0.1)
+        desc.fit = wl.fit.c()
         desc.arith = 0 if a.arith == "fast" else 1
         desc.kernel = a.kernel
         keep = []
+        if wl.axis_mask is not None:
+            m = np.ascontiguousarray(wl.axis_mask, np.uint8)
+            keep.append(m)
+            desc.axis_mask = m.ctypes.data
+            desc.flags = 0 if wl.fold else _abi.FLAG_NO_FOLD
         if wl.limit_weight:
             lo = np.ascontiguousarray(wl.soft_lo, np.float32)
             hi = np.ascontiguousarray(wl.soft_hi, np.float32)
