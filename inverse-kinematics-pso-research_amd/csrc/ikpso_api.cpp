@@ -273,6 +273,12 @@ ikpso_status parse_chain(const std::vector<ikpso_node>& nodes, const ikpso_pso_c
     for (int d = 0; d < 3 * J && ch.uniform_bounds; ++d)
         ch.uniform_bounds = ch.uniform_bounds && as_bits(ch.lo[d]) == as_bits(ch.lo[0]) &&
                             as_bits(ch.hi[d]) == as_bits(ch.hi[0]);
+    // [0, 2pi] limits are [0, 1] in revolutions (ChainConsts::rlo / rhi, the same fp32 products)
+    {
+        volatile float inv = 0.159154943091895336f;  // (no contraction or constant folding differences)
+        const float rlo = ch.lo[0] * inv, rhi = ch.hi[0] * inv;
+        ch.unit_rev_bounds = ch.uniform_bounds && rlo == 0.0f && rhi == 1.0f;
+    }
     ref7 = ref7 && eff_mask == 0xE0ull;                // effectors = nodes 5, 6, 7
     serial = serial && eff_mask == (1ull << J);        // single tip effector
     ch.topo = ref7 ? TopoKind::Ref7 : (serial ? TopoKind::SerialTip : TopoKind::Generic);

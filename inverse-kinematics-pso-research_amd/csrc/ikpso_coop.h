@@ -184,7 +184,7 @@ __global__ void __launch_bounds__(BLOCK, (BLOCK >= 256 ? BLOCK / 256 : 1))
         const int64_t b = cs.b;
         if (b >= io.num_swarms) break;
         const int i = cs.member * BLOCK + tid;  // particle index within the swarm
-        stage_swarm_inputs<Topo>(cc, io.targets, io.start_pose, b, sh);
+        stage_swarm_inputs<Topo, TERMS>(cc, io.targets, io.start_pose, b, sh);
         // the add-for-shift issue form only in the latency variant (one wave per
         // SIMD, room to spare): in the 2-wave serial-20 kernel it cost 5 %
         using Rng = XorwowT<BLOCK == kCoopLatencyThreads && std::is_same_v<RngFor<TERMS>, XorwowT<true>>>;
@@ -240,7 +240,7 @@ __global__ void __launch_bounds__(BLOCK, (BLOCK >= 256 ? BLOCK / 256 : 1))
         const int64_t bb = cs.b;
         const int ii = member * BLOCK + tid;
         if (member == 0) {  // outputs (updateGlobalBestCoordsKernel) + fitness + residual
-            store_angles<Topo>(cc, io.out_angles, bb, tid, tid < D ? sh.g[tid] : 0.0f);
+            store_angles<Topo, TERMS>(cc, io.out_angles, bb, tid, tid < D ? sh.g[tid] : 0.0f);
             if (tid == 0 && io.out_fitness) io.out_fitness[bb] = key_to_float(cs.gkey);
             if (io.out_residual && tid < 64) {
                 float g[D];
@@ -256,9 +256,9 @@ __global__ void __launch_bounds__(BLOCK, (BLOCK >= 256 ? BLOCK / 256 : 1))
                 float* base = io.dump_particles + bb * (int64_t)3 * D * P;
 #pragma unroll
                 for (int d = 0; d < D; ++d) {
-                    base[(int64_t)d * P + ii] = x[d];
-                    base[(int64_t)(D + d) * P + ii] = v[d];
-                    base[(int64_t)(2 * D + d) * P + ii] = s_pb[d * BLOCK + tid];
+                    base[(int64_t)d * P + ii] = radians<TERMS>(x[d]);
+                    base[(int64_t)(D + d) * P + ii] = radians<TERMS>(v[d]);
+                    base[(int64_t)(2 * D + d) * P + ii] = radians<TERMS>(s_pb[d * BLOCK + tid]);
                 }
             }
             if (io.dump_bests) io.dump_bests[bb * P + ii] = pbf;
@@ -314,13 +314,20 @@ inline hipError_t run_coop(const ChainHost& ch, const SwarmIO& io, hipStream_t s
     const ChainConsts<Topo::J> cc = make_consts<Topo::J>(ch);
     const int terms = term_set(ch);
     hipError_t err = hipSuccess;
-    if (dh_terms<Topo>(terms, &err,
-                       [&](auto t) { return launch_coop_kernel<Topo, MODE, decltype(t)::value>(cc, io, stream); }))
+    // angles in revolutions in the specialised FAST and folded-chain builds (kTermRev)
+    if (dh_terms<Topo>(terms, &err, [&](auto t) {
+            return launch_coop_kernel<Topo, MODE, decltype(t)::value | kTermRev>(cc, io, stream);
+        }))
         return err;
     if constexpr (!Topo::kGeneric && !Topo::kDH && MODE == IKPSO_ARITH_FAST) {
-        if (terms == kTermUniformBounds) return launch_coop_kernel<Topo, MODE, kTermUniformBounds>(cc, io, stream);
+        if constexpr (std::is_same_v<Topo, TopoRef7>) {  // the reference scene's [0, 2pi] limits
+            if (terms == kTermUniformBounds && ch.unit_rev_bounds)
+                return launch_coop_kernel<Topo, MODE, kTermUniformBounds | kTermRev | kTermUnitBounds>(cc, io, stream);
+        }
+        if (terms == kTermUniformBounds)
+            return launch_coop_kernel<Topo, MODE, kTermUniformBounds | kTermRev>(cc, io, stream);
         if (terms == (kTermUniformBounds | kTermPenalty))
-            return launch_coop_kernel<Topo, MODE, kTermUniformBounds | kTermPenalty>(cc, io, stream);
+            return launch_coop_kernel<Topo, MODE, kTermUniformBounds | kTermPenalty | kTermRev>(cc, io, stream);
     }
     return with_runtime_terms<Topo>(
         ch, [&](auto t) { return launch_coop_kernel<Topo, MODE, decltype(t)::value>(cc, io, stream); });

@@ -135,12 +135,20 @@ __host__ __device__ inline void xorwow_seed(uint64_t seed, uint32_t st[6])
 // flips.  Measured on gfx950 against correctly rounded sin/cos over 2^26
 // arguments in [-100, 100]: max 1 ulp, 71-73% correctly rounded
 // (tools/probes/trig_probe.hip).
-// HW: the transcendental unit instead (below).
-template <bool HW = false>
+// TRIG 1 (kTrigHw): the transcendental unit instead (below); TRIG 2 (kTrigHwRev):
+// the same with the angle given in revolutions (kTermRev kernels), so the
+// conversion multiply disappears.
+constexpr int kTrigPoly = 0, kTrigHw = 1, kTrigHwRev = 2;
+template <int HW = kTrigPoly>
 __host__ __device__ __forceinline__ void sincos_fast(float x, float* s_out, float* c_out)
 {
 #if defined(__HIP_DEVICE_COMPILE__)
-    if constexpr (HW) {
+    if constexpr (HW == kTrigHwRev) {
+        *s_out = __builtin_amdgcn_sinf(x);
+        *c_out = __builtin_amdgcn_cosf(x);
+        return;
+    }
+    if constexpr (HW == kTrigHw) {
         // v_sin_f32 / v_cos_f32 on x / 2pi (revolutions; the transcendental unit
         // reduces its own argument).  tools/probes/trig_probe.hip on gfx950: max
         // abs error 4.8e-7 on [0, 2pi] and 2.7e-7 on [-pi, pi] (vs 6e-8 for the
@@ -317,7 +325,7 @@ struct NodeTrig {
     float s[A], c[A];
 };
 
-template <bool HW, int A>
+template <int HW, int A>
 __device__ __forceinline__ NodeTrig<A> node_trig(const float* ang)
 {
     NodeTrig<A> t;
@@ -349,7 +357,7 @@ __device__ __forceinline__ Frame child_frame_fast_sc(const Frame& P, float sa, f
     return W;
 }
 
-template <bool HW>
+template <int HW>
 __device__ __forceinline__ Frame child_frame_fast(const Frame& P, float a, float b, float c, float len)
 {
     float sa, ca, sb, cb, sc, cc;
@@ -392,7 +400,7 @@ __device__ __forceinline__ Frame child_frame_fast_seq_sc(const Frame& P, float s
     return W;
 }
 
-template <bool HW>
+template <int HW>
 __device__ __forceinline__ Frame child_frame_fast_seq(const Frame& P, float a, float b, float c, float len)
 {
     float sa, ca, sb, cb, sc, cc;
@@ -445,9 +453,33 @@ __device__ __forceinline__ Frame child_frame_reference(const Frame& P, float a, 
     return W;
 }
 
+// FAST, a node whose parent is the origin, in the origin's own frame: R = Rx(a)
+// Ry(b) Rz(c) in closed form (14 operations instead of 36 that would rotate the
+// origin's columns) and p = len R e_x.  The kOriginFrame builds move the
+// targets into the origin frame at staging, t' = M0^T (t - p0): distances, and
+// with them the fitness and the residual, are unchanged by the rigid motion.
+__device__ __forceinline__ Frame root_frame_sc(float sa, float ca, float sb, float cb, float sc, float cc, float len)
+{
+    const float p = sa * sb, q = ca * sb;
+    Frame W;
+    W.r00 = cb * cc;
+    W.r01 = -cb * sc;
+    W.r02 = sb;
+    W.r10 = p * cc + ca * sc;
+    W.r11 = ca * cc - p * sc;
+    W.r12 = -sa * cb;
+    W.r20 = sa * sc - q * cc;
+    W.r21 = q * sc + sa * cc;
+    W.r22 = ca * cb;
+    W.px = len * W.r00;
+    W.py = len * W.r10;
+    W.pz = len * W.r20;
+    return W;
+}
+
 // SEQ: FAST mode may compose the rotation column-wise (interior nodes, or any
 // node whose full frame is consumed).  HW: FAST sin/cos on the transcendental unit.
-template <int MODE, bool SEQ = false, bool HW = false>
+template <int MODE, bool SEQ = false, int HW = kTrigPoly>
 __device__ __forceinline__ Frame child_frame(const Frame& P, float a, float b, float c, float len)
 {
     if constexpr (MODE == IKPSO_ARITH_REFERENCE)
@@ -477,8 +509,19 @@ __device__ __forceinline__ Frame child_frame(const Frame& P, float a, float b, f
 // kTermMask: the chain has a joint-axis mask (ChainConsts::free_mask): locked
 // angles take no draws and no update (uniform branches per dimension, which
 // cost the register allocator enough that unmasked chains get builds without).
+// kTermRev: the kernel keeps its angles in revolutions (x / 2pi): positions,
+// velocities, local and global bests, rest angles, clamp and soft limits, so the
+// transcendental unit's v_sin / v_cos take them as they are (kTrigHwRev: one
+// multiply fewer per angle); the angle and penalty weights carry the (2 pi)^2,
+// and the answers are scaled back by 2 pi on the way out.  Only the resident
+// and cooperative FAST builds with the hardware sin/cos (the streaming kernels
+// keep the reference's radian layout in HBM).
 constexpr int kTermPosRef = 1, kTermPenalty = 2, kTermRuntime = 4, kTermUniformBounds = 8, kTermColliders = 16,
-              kTermMask = 32;
+              kTermMask = 32, kTermRev = 64, kTermUnitBounds = 128;
+// kTermUnitBounds (with kTermRev and kTermUniformBounds): the clamp bounds are
+// exactly [0, 1] revolutions -- the reference scene's [0, 2pi] -- so the clamp
+// is the VALU's free output clamp on the position update instead of a v_med3
+// (half rate on gfx950).
 
 // Generator type of a swarm kernel: the add-for-shift issue form everywhere but
 // in the collider kernels, whose register allocation the opaque add perturbs
@@ -490,7 +533,36 @@ using RngFor = XorwowT<!(TERMS & kTermColliders)>;
 // this topology and term set: chains that run 4 waves per SIMD, no collider term
 // (whose contact decisions the tests compare across kernels bit for bit).
 template <class Topo, int MODE, int TERMS>
-constexpr bool kHwTrig = MODE == IKPSO_ARITH_FAST && !(TERMS & kTermColliders) && Topo::D <= 60;
+constexpr bool kHwTrigOk = MODE == IKPSO_ARITH_FAST && !(TERMS & kTermColliders) && Topo::D <= 60;
+// The sin/cos flavour of a kernel build (sincos_fast): polynomial, hardware on
+// radians, or hardware on revolutions (kTermRev).
+template <class Topo, int MODE, int TERMS>
+constexpr int kHwTrig = !kHwTrigOk<Topo, MODE, TERMS> ? kTrigPoly : (TERMS & kTermRev) ? kTrigHwRev : kTrigHw;
+template <class Topo, int MODE, int TERMS>
+constexpr bool kRev = (TERMS & kTermRev) != 0;
+// angle / penalty weights of a build (kTermRev: the (2 pi)^2 of the revolution units)
+template <int TERMS, class CC>
+__device__ __forceinline__ float angle_weight(const CC& cc) { return (TERMS & kTermRev) ? cc.aw_rev : cc.aw_j; }
+template <int TERMS, class CC>
+__device__ __forceinline__ float limit_weight(const CC& cc) { return (TERMS & kTermRev) ? cc.lim_rev : cc.lim_w; }
+constexpr float kInv2Pi = 0.159154943091895336f, k2Pi = 6.28318530717958648f;
+// the uniform clamp bounds (kTermUniformBounds) in the build's angle units
+// Euler topologies of the kTermRev builds evaluate their FK in the origin's
+// frame (root_frame_sc): the swarm kernels stage the targets moved into it.
+template <class Topo, int TERMS>
+constexpr bool kOriginFrame = (TERMS & kTermRev) && !Topo::kDH && !Topo::kGeneric;
+template <int TERMS, class CC>
+__device__ __forceinline__ float uniform_lo(const CC& cc)
+{
+    if constexpr (TERMS & kTermUnitBounds) return 0.0f;
+    return (TERMS & kTermRev) ? cc.rlo : cc.lo[0];
+}
+template <int TERMS, class CC>
+__device__ __forceinline__ float uniform_hi(const CC& cc)
+{
+    if constexpr (TERMS & kTermUnitBounds) return 1.0f;
+    return (TERMS & kTermRev) ? cc.rhi : cc.hi[0];
+}
 
 // Which kernel builds honour ChainConsts::free_mask (the host routes masked
 // chains to them; the folded chain has no locked angles).
@@ -529,11 +601,18 @@ struct FitnessAcc {
                                          const float* rest3, const float* tgt3, float* node_pos)
     {
         const int pk = Topo::kGeneric ? cc.parent[k] : Topo::parent(k);
-        constexpr bool HW = kHwTrig<Topo, MODE, TERMS>;
-        if (seq(k))
+        constexpr int HW = kHwTrig<Topo, MODE, TERMS>;
+        if (kOriginFrame<Topo, TERMS> && pk == 0) {
+            float sa, ca, sb, cb, sc, cc_;
+            sincos_fast<HW>(a, &sa, &ca);
+            sincos_fast<HW>(b, &sb, &cb);
+            sincos_fast<HW>(c, &sc, &cc_);
+            F[k] = root_frame_sc(sa, ca, sb, cb, sc, cc_, cc.len[k]);
+        } else if (seq(k)) {
             F[k] = child_frame<MODE, true, HW>(F[pk], a, b, c, cc.len[k]);
-        else
+        } else {
             F[k] = child_frame<MODE, false, HW>(F[pk], a, b, c, cc.len[k]);
+        }
         terms(cc, k, a, b, c, rest3, tgt3, node_pos);
     }
 
@@ -543,7 +622,9 @@ struct FitnessAcc {
     {
         static_assert(MODE == IKPSO_ARITH_FAST, "precomputed sin/cos: FAST arithmetic");
         const int pk = Topo::kGeneric ? cc.parent[k] : Topo::parent(k);
-        if (seq(k))
+        if (kOriginFrame<Topo, TERMS> && pk == 0)
+            F[k] = root_frame_sc(t.s[0], t.c[0], t.s[1], t.c[1], t.s[2], t.c[2], cc.len[k]);
+        else if (seq(k))
             F[k] = child_frame_fast_seq_sc(F[pk], t.s[0], t.c[0], t.s[1], t.c[1], t.s[2], t.c[2], cc.len[k]);
         else
             F[k] = child_frame_fast_sc(F[pk], t.s[0], t.c[0], t.s[1], t.c[1], t.s[2], t.c[2], cc.len[k]);
@@ -618,8 +699,9 @@ struct FitnessAcc {
     __device__ __forceinline__ float finish(const ChainConsts<J>& cc) const
     {
 #pragma clang fp contract(off)
-        float f = posref ? (distance + cc.dw_j * pos_diff) + cc.aw_j * rot_diff : distance + cc.aw_j * rot_diff;
-        if (penalty) f = f + cc.lim_w * pen;
+        const float aw = angle_weight<TERMS>(cc);
+        float f = posref ? (distance + cc.dw_j * pos_diff) + aw * rot_diff : distance + aw * rot_diff;
+        if (penalty) f = f + limit_weight<TERMS>(cc) * pen;
         if constexpr (TERMS & kTermColliders) f = hit ? FLT_MAX : f;
         return f;
     }
@@ -637,7 +719,7 @@ struct FitnessAcc {
 template <class Topo, int MODE, int TERMS>
 struct FitnessAccDH {
     static constexpr int J = Topo::J;
-    static constexpr bool HW = kHwTrig<Topo, MODE, TERMS>;
+    static constexpr int HW = kHwTrig<Topo, MODE, TERMS>;
     static_assert(MODE == IKPSO_ARITH_FAST, "the folded chain is FAST arithmetic only");
     const float* dhc;
     const float* soft;                                  // soft limits [lo 3J | hi 3J] (see FitnessAcc)
@@ -742,8 +824,8 @@ struct FitnessAccDH {
 
     __device__ __forceinline__ float finish(const ChainConsts<J>& cc) const
     {
-        float f = distance + cc.aw_j * rot_diff;
-        if (penalty) f = f + cc.lim_w * pen;
+        float f = distance + angle_weight<TERMS>(cc) * rot_diff;
+        if (penalty) f = f + limit_weight<TERMS>(cc) * pen;
         return f;
     }
 };
@@ -773,7 +855,7 @@ constexpr bool kTipBackward = MODE == IKPSO_ARITH_FAST &&
 template <class Topo, int MODE, int TERMS>
 struct TipBackAcc {
     static constexpr int J = Topo::J;
-    static constexpr bool HW = kHwTrig<Topo, MODE, TERMS>;
+    static constexpr int HW = kHwTrig<Topo, MODE, TERMS>;
     const float* soft;
     float rot_diff, pen, ux, uy, uz;
 
@@ -823,14 +905,17 @@ struct TipBackAcc {
     // fitness once back() has run for node 1: the tip term + the angle terms
     __device__ __forceinline__ float finish(const ChainConsts<J>& cc, const float* tgt3) const
     {
-        const float* m = cc.m0;  // origin frame, row-major 3x4
-        const float px = m[3] + (m[0] * ux + m[1] * uy + m[2] * uz);
-        const float py = m[7] + (m[4] * ux + m[5] * uy + m[6] * uz);
-        const float pz = m[11] + (m[8] * ux + m[9] * uy + m[10] * uz);
+        float px = ux, py = uy, pz = uz;  // kOriginFrame: the target is in the origin frame
+        if constexpr (!kOriginFrame<Topo, TERMS>) {
+            const float* m = cc.m0;  // origin frame, row-major 3x4
+            px = m[3] + (m[0] * ux + m[1] * uy + m[2] * uz);
+            py = m[7] + (m[4] * ux + m[5] * uy + m[6] * uz);
+            pz = m[11] + (m[8] * ux + m[9] * uy + m[10] * uz);
+        }
         const float ex = px - tgt3[0], ey = py - tgt3[1], ez = pz - tgt3[2];
         const float distance = ((ex * ex + ey * ey) + ez * ez) * cc.eff_w[J];
-        float f = distance + cc.aw_j * rot_diff;
-        if constexpr (TERMS & kTermPenalty) f = f + cc.lim_w * pen;
+        float f = distance + angle_weight<TERMS>(cc) * rot_diff;
+        if constexpr (TERMS & kTermPenalty) f = f + limit_weight<TERMS>(cc) * pen;
         return f;
     }
 };
@@ -842,7 +927,7 @@ struct TipBackAcc {
 template <class Topo, int MODE, int TERMS>
 struct TipBackAccDH {
     static constexpr int J = Topo::J;
-    static constexpr bool HW = kHwTrig<Topo, MODE, TERMS>;
+    static constexpr int HW = kHwTrig<Topo, MODE, TERMS>;
     const float* dhc;
     const float* soft;
     float rot_diff, pen, ux, uy, uz;
@@ -886,8 +971,8 @@ struct TipBackAccDH {
         const float px = dhc[12 * J + 0] + ux, py = dhc[12 * J + 1] + uy, pz = dhc[12 * J + 2] + uz;
         const float ex = px - tgt3[0], ey = py - tgt3[1], ez = pz - tgt3[2];
         const float distance = ((ex * ex + ey * ey) + ez * ez) * cc.eff_w[J];
-        float f = distance + cc.aw_j * rot_diff;
-        if constexpr (TERMS & kTermPenalty) f = f + cc.lim_w * pen;
+        float f = distance + angle_weight<TERMS>(cc) * rot_diff;
+        if constexpr (TERMS & kTermPenalty) f = f + limit_weight<TERMS>(cc) * pen;
         return f;
     }
 };
@@ -947,8 +1032,17 @@ __device__ __forceinline__ float residual(const ChainConsts<Topo::J>& cc, const 
 #pragma unroll
         for (int k = 1; k <= J; ++k) {
             const int pk = Topo::kGeneric ? cc.parent[k] : Topo::parent(k);
-            F[k] = child_frame<MODE, false, kHwTrig<Topo, MODE, TERMS>>(F[pk], x[3 * (k - 1)], x[3 * (k - 1) + 1],
-                                                                        x[3 * (k - 1) + 2], cc.len[k]);
+            constexpr int HW = kHwTrig<Topo, MODE, TERMS>;
+            if (kOriginFrame<Topo, TERMS> && pk == 0) {  // targets in the origin frame (kOriginFrame)
+                float sa, ca, sb, cb, sc, cc_;
+                sincos_fast<HW>(x[3 * (k - 1)], &sa, &ca);
+                sincos_fast<HW>(x[3 * (k - 1) + 1], &sb, &cb);
+                sincos_fast<HW>(x[3 * (k - 1) + 2], &sc, &cc_);
+                F[k] = root_frame_sc(sa, ca, sb, cb, sc, cc_, cc.len[k]);
+            } else {
+                F[k] = child_frame<MODE, false, HW>(F[pk], x[3 * (k - 1)], x[3 * (k - 1) + 1], x[3 * (k - 1) + 2],
+                                                    cc.len[k]);
+            }
             if (Topo::effector(k) && cc.eff_slot[k] >= 0) {
                 const float dx = tgt[3 * (k - 1) + 0] - F[k].px;
                 const float dy = tgt[3 * (k - 1) + 1] - F[k].py;

@@ -59,6 +59,7 @@ struct ChainHost {
     float w = 0, c1 = 0, c2 = 0, aw_j = 0, dw_j = 0, lim_w = 0;
     bool use_posref = false, use_penalty = false;
     bool uniform_bounds = false;  // every angle has clamp bounds lo[0], hi[0]
+    bool unit_rev_bounds = false; // ... and they are [0, 1] in revolutions (kTermUnitBounds): [0, 2pi]
     int num_coll = 0;             // colliders (obj_t) of the scene
     size_t coll_off = 0;          // float offset of the collider records in aux
     // joint-axis mask over the kernel's dimensions (all set: no mask) and the
@@ -154,6 +155,10 @@ ChainConsts<J> make_consts(const ChainHost& h)
     c.aw_j = h.aw_j;
     c.dw_j = h.dw_j;
     c.lim_w = h.lim_w;
+    c.aw_rev = h.aw_j * 39.4784176043574344f;  // (2 pi)^2
+    c.lim_rev = h.lim_w * 39.4784176043574344f;
+    c.rlo = h.lo.empty() ? 0.0f : h.lo[0] * 0.159154943091895336f;
+    c.rhi = h.hi.empty() ? 0.0f : h.hi[0] * 0.159154943091895336f;
     c.use_posref = h.use_posref ? 1 : 0;
     c.use_penalty = h.use_penalty ? 1 : 0;
     c.num_eff = h.E;

@@ -31,6 +31,9 @@ struct ChainConsts {
     float wq, c1q, c2q;       // the same times 2^-32 (exact): FAST mode folds
     float wh, c1h, c2h;       // the uniform's affine map, times 2^-33 (exact)
     float aw_j, dw_j, lim_w;  // angleWeight/J, distanceWeight/J, limit weight
+    // kTermRev builds (angles in revolutions): the weights times (2 pi)^2 and the
+    // uniform clamp bounds over 2 pi
+    float aw_rev, lim_rev, rlo, rhi;
     int32_t use_posref, use_penalty;
     int32_t num_eff;
     int32_t num_coll;         // colliders (kTermColliders kernels only)

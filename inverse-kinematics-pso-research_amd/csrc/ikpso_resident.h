@@ -78,7 +78,7 @@ __device__ __forceinline__ void update_node(const ChainConsts<Topo::J>& cc, cons
         if (kMasked<Topo, TERMS> && !dim_free(cc, d)) continue;  // locked: stays at rest
         pso_update<MODE>(x[d], v[d], s_pb[d * BLOCK + tid], sh.g[d], coef, rng);
         if constexpr (TERMS & kTermUniformBounds)
-            x[d] = clamp_mode<MODE>(x[d], cc.lo[0], cc.hi[0]);
+            x[d] = clamp_mode<MODE>(x[d], uniform_lo<TERMS>(cc), uniform_hi<TERMS>(cc));
         else
             x[d] = clamp_mode<MODE>(x[d], sh.lo[d], sh.hi[d]);
     }
@@ -94,7 +94,7 @@ __device__ __forceinline__ float swarm_step_ahead(const ChainConsts<Topo::J>& cc
                                                   const PsoCoef& coef, Rng& rng)
 {
     constexpr int J = Topo::J, A = Topo::A;
-    constexpr bool HW = kHwTrig<Topo, MODE, TERMS>;
+    constexpr int HW = kHwTrig<Topo, MODE, TERMS>;
     FitnessFor<Topo, MODE, TERMS> acc(cc, sh.dh, sh.soft);
     progress_prio<J, kPrioLevels4Wave>(1);
     update_node<Topo, MODE, TERMS, BLOCK>(cc, sh, s_pb, tid, 1, x, v, coef, rng);
@@ -164,7 +164,7 @@ __device__ __forceinline__ void swarm_step_tip(const ChainConsts<Topo::J>& cc, S
             const int d = A * (k - 1) + ax;
             pso_update<MODE>(x[d], v[d], cpb[ax], cg[ax], coef, rng);
             if constexpr (TERMS & kTermUniformBounds)
-                x[d] = clamp_mode<MODE>(x[d], cc.lo[0], cc.hi[0]);
+                x[d] = clamp_mode<MODE>(x[d], uniform_lo<TERMS>(cc), uniform_hi<TERMS>(cc));
             else
                 x[d] = clamp_mode<MODE>(x[d], sh.lo[d], sh.hi[d]);
         }
@@ -256,7 +256,7 @@ __device__ __forceinline__ void swarm_step(const ChainConsts<Topo::J>& cc, Swarm
             if (MASK && !dim_free(cc, d)) continue;  // locked: stays at rest
             pso_update<MODE>(x[d], v[d], cpb[ax], cg[ax], coef, rng);
             if constexpr (TERMS & kTermUniformBounds)
-                x[d] = clamp_mode<MODE>(x[d], cc.lo[0], cc.hi[0]);
+                x[d] = clamp_mode<MODE>(x[d], uniform_lo<TERMS>(cc), uniform_hi<TERMS>(cc));
             else
                 x[d] = clamp_mode<MODE>(x[d], sh.lo[d], sh.hi[d]);
         }
@@ -286,6 +286,8 @@ __device__ __forceinline__ void init_particle(const ChainConsts<Topo::J>& cc, co
         x[d] = sh.rest[d];
         if (kMasked<Topo, TERMS> && !dim_free(cc, d))
             v[d] = 0.0f;
+        else if constexpr (TERMS & kTermRev)  // (U * 2 - 1) / 2pi
+            v[d] = __builtin_fmaf(rng.uniform(), 0.318309886183790672f, -kInv2Pi);
         else
             v[d] = __builtin_fmaf(rng.uniform(), 2.0f, -1.0f);
         s_pb[d * BLOCK + tid] = x[d];
@@ -307,7 +309,7 @@ __device__ __forceinline__ void swarm_resident_body(const ChainConsts<Topo::J>& 
     const int P = io.P;
     const bool active = tid < P;
 
-    stage_swarm_inputs<Topo>(cc, io.targets, io.start_pose, b, sh);
+    stage_swarm_inputs<Topo, TERMS>(cc, io.targets, io.start_pose, b, sh);
 
     RngFor<TERMS> rng{0, 0, 0, 0, 0, 0};
     if (active) load_rng(rng, io.rng + b * P + tid);
@@ -341,7 +343,7 @@ __device__ __forceinline__ void swarm_resident_body(const ChainConsts<Topo::J>& 
 
     // outputs: Coordinates result (updateGlobalBestCoordsKernel) + fitness + residual
     compiler_fence();
-    store_angles<Topo>(cc, io.out_angles, b, tid, tid < D ? sh.g[tid] : 0.0f);
+    store_angles<Topo, TERMS>(cc, io.out_angles, b, tid, tid < D ? sh.g[tid] : 0.0f);
     if (tid == 0 && io.out_fitness) io.out_fitness[b] = key_to_float(gkey);
     if (io.out_residual && tid < 64) {
         float g[D];
@@ -356,9 +358,9 @@ __device__ __forceinline__ void swarm_resident_body(const ChainConsts<Topo::J>& 
             float* base = io.dump_particles + b * (int64_t)3 * D * P;
 #pragma unroll
             for (int d = 0; d < D; ++d) {
-                base[(int64_t)d * P + tid] = x[d];
-                base[(int64_t)(D + d) * P + tid] = v[d];
-                base[(int64_t)(2 * D + d) * P + tid] = s_pb[d * BLOCK + tid];
+                base[(int64_t)d * P + tid] = radians<TERMS>(x[d]);
+                base[(int64_t)(D + d) * P + tid] = radians<TERMS>(v[d]);
+                base[(int64_t)(2 * D + d) * P + tid] = radians<TERMS>(s_pb[d * BLOCK + tid]);
             }
         }
         if (io.dump_bests) io.dump_bests[b * P + tid] = pbf;
@@ -447,21 +449,32 @@ inline hipError_t run_resident(const ChainHost& ch, const SwarmIO& io, int block
     // kernels; everything else (generic topologies, the distance term, every
     // REFERENCE-mode run) tests the terms at run time with the same arithmetic,
     // with the collider block compiled in only when the scene has colliders.
+    // The specialised FAST builds (and every folded-chain build) keep their
+    // angles in revolutions (kTermRev).
     const int terms = term_set(ch);
     hipError_t err = hipSuccess;
     if (dh_terms<Topo>(terms, &err, [&](auto t) {
-            hipLaunchKernelGGL((k_swarm_resident<Topo, MODE, decltype(t)::value>), grid, threads, 0, stream, cc, io);
+            hipLaunchKernelGGL((k_swarm_resident<Topo, MODE, decltype(t)::value | kTermRev>), grid, threads, 0, stream,
+                               cc, io);
             return hipGetLastError();
         }))
         return err;
     if constexpr (!Topo::kGeneric && !Topo::kDH && MODE == IKPSO_ARITH_FAST) {
+        if constexpr (std::is_same_v<Topo, TopoRef7>) {  // the reference scene's [0, 2pi] limits
+            if (terms == kTermUniformBounds && ch.unit_rev_bounds) {
+                hipLaunchKernelGGL((k_swarm_resident<Topo, MODE, kTermUniformBounds | kTermRev | kTermUnitBounds>),
+                                   grid, threads, 0, stream, cc, io);
+                return hipGetLastError();
+            }
+        }
         if (terms == kTermUniformBounds) {
-            hipLaunchKernelGGL((k_swarm_resident<Topo, MODE, kTermUniformBounds>), grid, threads, 0, stream, cc, io);
+            hipLaunchKernelGGL((k_swarm_resident<Topo, MODE, kTermUniformBounds | kTermRev>), grid, threads, 0, stream,
+                               cc, io);
             return hipGetLastError();
         }
         if (terms == (kTermUniformBounds | kTermPenalty)) {
-            hipLaunchKernelGGL((k_swarm_resident<Topo, MODE, kTermUniformBounds | kTermPenalty>), grid, threads, 0,
-                               stream, cc, io);
+            hipLaunchKernelGGL((k_swarm_resident<Topo, MODE, kTermUniformBounds | kTermPenalty | kTermRev>), grid,
+                               threads, 0, stream, cc, io);
             return hipGetLastError();
         }
     }

@@ -67,33 +67,64 @@ struct SwarmLds {
 };
 
 // start_pose: [B][dfree] over the free dimensions (the chain's mask).
-template <class Topo>
+// kTermRev builds: the angles (rest pose, clamp and soft limits) in revolutions.
+template <class Topo, int TERMS = 0>
 __device__ __forceinline__ void stage_swarm_inputs(const ChainConsts<Topo::J>& cc, const float* targets,
                                                    const float* start_pose, int64_t b, SwarmShared<Topo>& sh)
 {
     constexpr int D = Topo::D, J = Topo::J;
+    constexpr float sc = (TERMS & kTermRev) ? kInv2Pi : 1.0f;
     const float* t = targets ? targets + b * (int64_t)cc.num_eff * 3 : nullptr;
     for (int d = threadIdx.x; d < D; d += blockDim.x) {
-        sh.lo[d] = cc.lo[d];
-        sh.hi[d] = cc.hi[d];
-        sh.rest[d] = start_pose && dim_free(cc, d) ? start_pose[b * cc.dfree + dim_rank(cc, d)] : cc.rest[d];
+        sh.lo[d] = cc.lo[d] * sc;
+        sh.hi[d] = cc.hi[d] * sc;
+        sh.rest[d] = (start_pose && dim_free(cc, d) ? start_pose[b * cc.dfree + dim_rank(cc, d)] : cc.rest[d]) * sc;
     }
-    for (int n = threadIdx.x; n < 3 * J; n += blockDim.x) {
-        const int s = cc.eff_slot[n / 3 + 1];
-        sh.tgt[n] = t ? (s >= 0 ? t[3 * s + n % 3] : 0.0f) : cc.tgt0[n];
+    if constexpr (kOriginFrame<Topo, TERMS>) {
+        // targets moved into the origin's frame: t' = M0^T (t - p0) (root_frame_sc)
+        const float* m = cc.m0;
+        for (int k = threadIdx.x; k < J; k += blockDim.x) {
+            const int s = cc.eff_slot[k + 1];
+            float w[3];
+#pragma unroll
+            for (int c = 0; c < 3; ++c) w[c] = (t ? (s >= 0 ? t[3 * s + c] : 0.0f) : cc.tgt0[3 * k + c]) - m[4 * c + 3];
+#pragma unroll
+            for (int c = 0; c < 3; ++c)
+                sh.tgt[3 * k + c] = s >= 0 ? m[c] * w[0] + m[4 + c] * w[1] + m[8 + c] * w[2] : 0.0f;
+        }
+    } else {
+        for (int n = threadIdx.x; n < 3 * J; n += blockDim.x) {
+            const int s = cc.eff_slot[n / 3 + 1];
+            sh.tgt[n] = t ? (s >= 0 ? t[3 * s + n % 3] : 0.0f) : cc.tgt0[n];
+        }
     }
     if constexpr (Topo::kDH)
         for (int n = threadIdx.x; n < 12 * J + 4; n += blockDim.x) sh.dh[n] = cc.aux[cc.dh_off + n];
     if (cc.use_penalty)
-        for (int n = threadIdx.x; n < 6 * J; n += blockDim.x) sh.soft[n] = cc.aux[4 * J + n];
+        for (int n = threadIdx.x; n < 6 * J; n += blockDim.x) sh.soft[n] = cc.aux[4 * J + n] * sc;
+}
+
+// An angle of the kernel's units in radians (kTermRev: revolutions * 2 pi).
+template <int TERMS>
+__device__ __forceinline__ float radians(float a)
+{
+    if constexpr (TERMS & kTermRev)
+        return a * k2Pi;
+    else
+        return a;
 }
 
 // The swarm's answer over the free dimensions: out[b][dfree] from the kernel's
 // D-vector g (every thread of the calling workgroup; lanes < D write).
-template <class Topo>
+// kTermRev builds: g in revolutions, scaled back to radians and held inside the
+// clamp bounds (a bound's round trip through revolutions may land an ulp out).
+template <class Topo, int TERMS = 0>
 __device__ __forceinline__ void store_angles(const ChainConsts<Topo::J>& cc, float* out, int64_t b, int d, float g)
 {
-    if (d < Topo::D && dim_free(cc, d)) out[b * cc.dfree + dim_rank(cc, d)] = g;
+    if (d < Topo::D && dim_free(cc, d)) {
+        if constexpr (TERMS & kTermRev) g = fminf(fmaxf(g * k2Pi, cc.lo[d]), cc.hi[d]);
+        out[b * cc.dfree + dim_rank(cc, d)] = g;
+    }
 }
 
 __device__ __forceinline__ void compiler_fence() { asm volatile("" ::: "memory"); }

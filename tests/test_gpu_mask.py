@@ -169,7 +169,7 @@ def test_folded_chain_one_pose(oracle, device):
     start = (rng.uniform(-1, 1, (B, 7)) * LIM + arm.z_offset).astype(np.float32)
     (ang, fit, res), name, _ = solve(chain, mask, tg, 64, 0, "fast", start=start)
     assert "dh7" in name
-    assert np.array_equal(ang, start)
+    np.testing.assert_array_max_ulp(ang, start, 4)  # the start pose through revolutions (kTermRev)
     fd = oracle.free_dims(chain, mask)
     for b in range(B):
         c = chain.copy()
