@@ -319,6 +319,18 @@ ikpso_status parse_chain(const std::vector<ikpso_node>& nodes, const ikpso_pso_c
         if ((ch.free_mask >> d) & 1)
             ch.poly_trig = ch.poly_trig || !(fabsf(ch.lo[d]) <= kHwTrigMaxAbs) || !(fabsf(ch.hi[d]) <= kHwTrigMaxAbs) ||
                            !(fabsf(ch.rest[d]) <= kHwTrigMaxAbs);
+    // symmetric soft limits within one revolution of every clamp bound (kTermSymPenalty): checked in the
+    // kernels' revolution units, where the overshoot |x| - h of a clamped angle is <= 1
+    if (ch.use_penalty && ch.uniform_bounds) {
+        volatile float inv = 0.159154943091895336f;
+        const float rmax = fmaxf(fabsf(ch.lo[0] * inv), fabsf(ch.hi[0] * inv));
+        ch.sym_penalty = true;
+        for (int d = 0; d < 3 * J; ++d) {
+            const float slo = ch.aux[4 * J + d], shi = ch.aux[7 * J + d];
+            ch.sym_penalty = ch.sym_penalty && as_bits(slo) == (as_bits(shi) ^ 0x80000000u) && shi >= 0.0f &&
+                             rmax - shi * inv <= 1.0f;
+        }
+    }
     if (!chain_supported(ch)) return IKPSO_ERR_UNSUPPORTED;
     return IKPSO_OK;
 }

@@ -79,9 +79,13 @@ struct CoopShared {
 // chunks, reduce; returns the group-wide minimum key of this exchange (uniform)
 // and leaves the winner's local best in sh.g when it improves on `gkey` (or
 // always when `force`).  Called by every wave; wave 0 does the global work.
-template <class Topo, int BLOCK>
+// ahead(): gbest-independent work of the next iteration, done while the
+// exchange is in flight (wave 0 between its publish and its poll, the other
+// waves while wave 0 hands off) when do_ahead.
+template <class Topo, int BLOCK, class AheadFn>
 __device__ __forceinline__ void coop_exchange(SwarmShared<Topo>& sh, CoopShared<Topo::J>& cs, const float* s_pb,
-                                              uint32_t local_key, int32_t* error, uint32_t spin_limit, bool force)
+                                              uint32_t local_key, int32_t* error, uint32_t spin_limit, bool force,
+                                              bool do_ahead, AheadFn&& ahead)
 {
     constexpr int D = Topo::D;
     constexpr int SLOT = kCoopSlot(D);
@@ -101,6 +105,7 @@ __device__ __forceinline__ void coop_exchange(SwarmShared<Topo>& sh, CoopShared<
         // granule 0: the key; granules 1..D: the chunk winner's local best
         const float mine_d = lane >= 1 && lane <= D ? s_pb[(lane - 1) * BLOCK + lidx] : 0.0f;
         if (lane <= D) st_granule(base + (size_t)member * SLOT + lane, tag | (lane == 0 ? lmin : __float_as_uint(mine_d)));
+        if (do_ahead) ahead();
         // the G key granules, in chunk order (lanes 0..G-1; G <= 64)
         uint32_t n = 0;
         int timed_out = 0;
@@ -142,9 +147,21 @@ __device__ __forceinline__ void coop_exchange(SwarmShared<Topo>& sh, CoopShared<
                 __hip_atomic_store(error, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
         }
+    } else if (do_ahead) {
+        ahead();
     }
     __syncthreads();
 }
+
+// Dimensions of the next iteration's update drawn ahead during the exchange,
+// in the throughput build of the FAST tip-backward (long-chain, 2-wave) step:
+// wave 0 draws them between its publish and its poll, the other waves while
+// wave 0 hands off, so the hand-off's wait carries work.  Config 5, 2048 swarms
+// x 4096 x 100: 3 dimensions (node 1) 64.4 -> 63.3 ms; 6 and 9 measured no
+// better than 3 (the extra live values cost the step more than the window saves:
+// profiles/r03b, r03c variant_timings).
+template <class Topo, int MODE, int TERMS, int BLOCK>
+constexpr int kCoopAhead = (kTipBackward<Topo, MODE, TERMS> && BLOCK != kCoopLatencyThreads && Topo::D > 30) ? 3 : 0;
 
 // BLOCK: kCoopThreads<D>() (throughput: fill each CU), or kCoopLatencyThreads
 // for a few swarms (latency: one wave per SIMD on 4x more CUs).
@@ -196,10 +213,17 @@ __global__ void __launch_bounds__(BLOCK, (BLOCK >= 256 ? BLOCK / 256 : 1))
         // initParticlesKernel + initLocalBests (src/kernel.cu:191-266)
         float x[D], v[D];
         init_particle<Topo, TERMS, BLOCK>(cc, sh, s_pb, tid, x, v, rng);
+        // the next iteration's first KA dimensions drawn ahead, inside the exchange
+        constexpr int KA = kCoopAhead<Topo, MODE, TERMS, BLOCK>;
+        float pa[KA > 0 ? KA : 1], pc[KA > 0 ? KA : 1];
+        auto ahead = [&]() {
+#pragma unroll
+            for (int d = 0; d < KA; ++d) pso_draw_ahead(pa[d], pc[d], x[d], v[d], s_pb[d * BLOCK + tid], coef, rng);
+        };
         float pbf = fitness<Topo, MODE, TERMS>(cc, x, sh.rest, sh.tgt, nullptr, sh.dh, sh.soft);
         // swarm argmin + unconditional first global-best copy (src/kernel.cu:297-304)
         const uint32_t key0 = i < P ? ordered_key(pbf) : 0xFFFFFFFFu;
-        coop_exchange<Topo, BLOCK>(sh, cs, s_pb, key0, io.coop_error, io.coop_spin_limit, true);
+        coop_exchange<Topo, BLOCK>(sh, cs, s_pb, key0, io.coop_error, io.coop_spin_limit, true, io.iterations > 0, ahead);
 
 #if IKPSO_COOP_TIMING
         unsigned long long t_step = 0, t_bar = 0, t_exch = 0, n_it = 0;
@@ -210,13 +234,17 @@ __global__ void __launch_bounds__(BLOCK, (BLOCK >= 256 ? BLOCK / 256 : 1))
 #if IKPSO_COOP_TIMING
             const unsigned long long t0 = __builtin_amdgcn_s_memtime();
 #endif
-            swarm_step<Topo, MODE, TERMS, BLOCK>(cc, sh, s_pb, tid, x, v, pbf, coef, rng);
+            if constexpr (KA > 0)
+                swarm_step_tip<Topo, MODE, TERMS, BLOCK, KA>(cc, sh, s_pb, tid, x, v, pbf, coef, rng, pa, pc);
+            else
+                swarm_step<Topo, MODE, TERMS, BLOCK>(cc, sh, s_pb, tid, x, v, pbf, coef, rng);
             const bool act = cs.member * BLOCK + tid < P;
             const uint32_t key = act ? ordered_key(pbf) : 0xFFFFFFFFu;
 #if IKPSO_COOP_TIMING
             const unsigned long long t1 = __builtin_amdgcn_s_memtime();
 #endif
-            coop_exchange<Topo, BLOCK>(sh, cs, s_pb, key, io.coop_error, io.coop_spin_limit, false);
+            coop_exchange<Topo, BLOCK>(sh, cs, s_pb, key, io.coop_error, io.coop_spin_limit, false,
+                                       it + 1 < io.iterations, ahead);
 #if IKPSO_COOP_TIMING
             const unsigned long long t2 = __builtin_amdgcn_s_memtime();
             t_step += t1 - t0;  // wave 0's own step
@@ -326,6 +354,11 @@ inline hipError_t run_coop(const ChainHost& ch, const SwarmIO& io, hipStream_t s
         }
         if (terms == kTermUniformBounds)
             return launch_coop_kernel<Topo, MODE, kTermUniformBounds | kTermRev>(cc, io, stream);
+        if constexpr (std::is_same_v<Topo, TopoSerialTip<20>>) {  // BASELINE config 5's symmetric soft limits
+            if (terms == (kTermUniformBounds | kTermPenalty) && ch.sym_penalty)
+                return launch_coop_kernel<Topo, MODE, kTermUniformBounds | kTermPenalty | kTermRev | kTermSymPenalty>(
+                    cc, io, stream);
+        }
         if (terms == (kTermUniformBounds | kTermPenalty))
             return launch_coop_kernel<Topo, MODE, kTermUniformBounds | kTermPenalty | kTermRev>(cc, io, stream);
     }

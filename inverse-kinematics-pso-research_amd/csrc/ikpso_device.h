@@ -517,11 +517,16 @@ __device__ __forceinline__ Frame child_frame(const Frame& P, float a, float b, f
 // and cooperative FAST builds with the hardware sin/cos (the streaming kernels
 // keep the reference's radian layout in HBM).
 constexpr int kTermPosRef = 1, kTermPenalty = 2, kTermRuntime = 4, kTermUniformBounds = 8, kTermColliders = 16,
-              kTermMask = 32, kTermRev = 64, kTermUnitBounds = 128;
+              kTermMask = 32, kTermRev = 64, kTermUnitBounds = 128, kTermSymPenalty = 256;
 // kTermUnitBounds (with kTermRev and kTermUniformBounds): the clamp bounds are
 // exactly [0, 1] revolutions -- the reference scene's [0, 2pi] -- so the clamp
 // is the VALU's free output clamp on the position update instead of a v_med3
 // (half rate on gfx950).
+// kTermSymPenalty (with kTermRev and kTermPenalty): the soft limits are
+// symmetric, soft_lo = -soft_hi, and every clamped angle lies within one
+// revolution of them, so the penalty's overshoot max(|x| - h, 0) is the VALU's
+// free output clamp of |x| - h (<= 1) instead of two subtractions and a v_max3
+// (half rate): BASELINE config 5's +-pi/2 soft limits inside +-pi.
 
 // Generator type of a swarm kernel: the add-for-shift issue form everywhere but
 // in the collider kernels, whose register allocation the opaque add perturbs
@@ -870,8 +875,11 @@ struct TipBackAcc {
 #pragma unroll
             for (int ax = 0; ax < 3; ++ax) {
                 const int d = 3 * (k - 1) + ax;
-                const float slo = soft[d], shi = soft[3 * J + d];
-                const float over = fmaxf(fmaxf(ang[ax] - shi, slo - ang[ax]), 0.0f);
+                float over;
+                if constexpr (TERMS & kTermSymPenalty)  // |x| - h clamped to [0, 1]: one v_sub with clamp
+                    over = __builtin_amdgcn_fmed3f(fabsf(ang[ax]) - soft[3 * J + d], 0.0f, 1.0f);
+                else
+                    over = fmaxf(fmaxf(ang[ax] - soft[3 * J + d], soft[d] - ang[ax]), 0.0f);
                 pen = pen + over * over;
             }
         }
@@ -1093,6 +1101,25 @@ __device__ __forceinline__ void pso_update(float& x, float& v, float pb, float g
         v = __builtin_fmaf(a, v, __builtin_fmaf(b, pb - x, c * (g - x)));
         x += v;
     }
+}
+
+// FAST: the gbest-independent part of one dimension's update drawn ahead (the
+// next iteration's r1, r2, r3, in the same order): pa = w r1 v + c1 r2 (pb - x),
+// pc = c2 r3; the update then completes as v = pc (g - x) + pa once the new
+// global best is known (pso_update_ahead).
+template <class Rng>
+__device__ __forceinline__ void pso_draw_ahead(float& pa, float& pc, float x, float v, float pb, const PsoCoef& k,
+                                               Rng& rng)
+{
+    const float a = rng.scaled(k.wq, k.wh);
+    const float b = rng.scaled(k.c1q, k.c1h);
+    pc = rng.scaled(k.c2q, k.c2h);
+    pa = __builtin_fmaf(a, v, b * (pb - x));
+}
+__device__ __forceinline__ void pso_update_ahead(float& x, float& v, float g, float pa, float pc)
+{
+    v = __builtin_fmaf(pc, g - x, pa);
+    x += v;
 }
 
 // clamp (src/matrix_operations.cuh:187-190)

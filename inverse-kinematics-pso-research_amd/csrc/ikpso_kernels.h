@@ -60,6 +60,7 @@ struct ChainHost {
     bool use_posref = false, use_penalty = false;
     bool uniform_bounds = false;  // every angle has clamp bounds lo[0], hi[0]
     bool unit_rev_bounds = false; // ... and they are [0, 1] in revolutions (kTermUnitBounds): [0, 2pi]
+    bool sym_penalty = false;     // soft limits symmetric and within a revolution of the clamp (kTermSymPenalty)
     int num_coll = 0;             // colliders (obj_t) of the scene
     size_t coll_off = 0;          // float offset of the collider records in aux
     // joint-axis mask over the kernel's dimensions (all set: no mask) and the

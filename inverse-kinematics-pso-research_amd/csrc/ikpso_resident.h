@@ -124,10 +124,11 @@ __device__ __forceinline__ float swarm_step_ahead(const ChainConsts<Topo::J>& cc
 // angle terms in node order), then the tip is evaluated from the tip back
 // (TipAccFor), each node's sines and cosines computed one node ahead of its
 // rotation.
-template <class Topo, int MODE, int TERMS, int BLOCK, class Rng>
+template <class Topo, int MODE, int TERMS, int BLOCK, int KA = 0, class Rng>
 __device__ __forceinline__ void swarm_step_tip(const ChainConsts<Topo::J>& cc, SwarmShared<Topo>& sh, float* s_pb,
                                                int tid, float (&x)[Topo::D], float (&v)[Topo::D], float& pbf,
-                                               const PsoCoef& coef, Rng& rng)
+                                               const PsoCoef& coef, Rng& rng, const float* pa = nullptr,
+                                               const float* pc = nullptr)
 {
     constexpr int J = Topo::J, A = Topo::A, D = Topo::D;
     constexpr int PL = D > kTrigAheadMaxD ? kPrioLevels2Wave : 0;  // wave priority: the 2-wave kernels
@@ -162,7 +163,10 @@ __device__ __forceinline__ void swarm_step_tip(const ChainConsts<Topo::J>& cc, S
 #pragma unroll
         for (int ax = 0; ax < A; ++ax) {
             const int d = A * (k - 1) + ax;
-            pso_update<MODE>(x[d], v[d], cpb[ax], cg[ax], coef, rng);
+            if (d < KA)  // drawn ahead during the previous exchange (k_swarm_coop)
+                pso_update_ahead(x[d], v[d], cg[ax], pa[d], pc[d]);
+            else
+                pso_update<MODE>(x[d], v[d], cpb[ax], cg[ax], coef, rng);
             if constexpr (TERMS & kTermUniformBounds)
                 x[d] = clamp_mode<MODE>(x[d], uniform_lo<TERMS>(cc), uniform_hi<TERMS>(cc));
             else
@@ -471,6 +475,14 @@ inline hipError_t run_resident(const ChainHost& ch, const SwarmIO& io, int block
             hipLaunchKernelGGL((k_swarm_resident<Topo, MODE, kTermUniformBounds | kTermRev>), grid, threads, 0, stream,
                                cc, io);
             return hipGetLastError();
+        }
+        if constexpr (std::is_same_v<Topo, TopoSerialTip<20>>) {  // BASELINE config 5's symmetric soft limits
+            if (terms == (kTermUniformBounds | kTermPenalty) && ch.sym_penalty) {
+                hipLaunchKernelGGL(
+                    (k_swarm_resident<Topo, MODE, kTermUniformBounds | kTermPenalty | kTermRev | kTermSymPenalty>),
+                    grid, threads, 0, stream, cc, io);
+                return hipGetLastError();
+            }
         }
         if (terms == (kTermUniformBounds | kTermPenalty)) {
             hipLaunchKernelGGL((k_swarm_resident<Topo, MODE, kTermUniformBounds | kTermPenalty | kTermRev>), grid,

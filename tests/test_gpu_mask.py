@@ -256,3 +256,32 @@ def test_dh_arm_masked_solves_reachable_targets(device):
     assert np.median(err) < 1e-3 and np.mean(err < 1e-2) >= 0.9, err
     th = np.array([arm.joint_angles(a) for a in ang])
     assert np.all(np.abs(th) <= LIM + 1e-5)
+
+
+def test_dh7_bench_workload_tier_b(oracle, device):
+    """Tier B on the benchmarked DH workload itself (bench.py --config dh7: the
+    iiwa arm, reachable targets, position-only fitness, 1024 particles, 500
+    iterations), 64 swarms, FAST folded chain vs the oracle's masked Euler solve.
+    The oracle drives every swarm's tip onto its target to fp32 resolution
+    (residual median 0, max 3.7e-9 on these 64 swarms); so must the GPU: its own
+    residual <= 1e-5 on every swarm, and the reference FK (oracle) of its answers
+    within 1e-4 of the target (the folded constants are fp32-rounded products, so
+    the two FKs of one pose differ by ~1e-6)."""
+    wl = ikpso.workload("dh7")
+    B, P, I = 64, wl.particles, wl.iterations
+    tg = wl.targets(0, B)
+    s = ikpso.BatchSolver(wl.chain, P, pso=wl.pso, fit=wl.fit, axis_mask=wl.axis_mask)
+    assert "dh7" in s.kernel
+    s.seed(B)
+    ang, fit, res = (t.cpu().numpy() for t in s.solve(dev(tg), iterations=I))
+    s.close()
+    ostate = oracle.init_generators(B * P, 0)
+    oang, ofit, ores = oracle.solve_batch(wl.chain, tg, None, P, I, ostate, threads=0, axis_mask=wl.axis_mask,
+                                          angle_weight=wl.fit.angle_weight)
+    assert ores.max() <= 1e-5
+    assert np.isfinite(ang).all() and res.max() <= 1e-5, np.sort(res)[-4:]
+    for b in range(B):
+        c = wl.chain.copy()
+        c["target_position"][-1] = tg[b, 0]
+        full = oracle.expand(c, ang[b], wl.axis_mask)
+        assert oracle.residual(c, full) <= 1e-4, (b, oracle.residual(c, full))
