@@ -502,7 +502,7 @@ int env_kernel()
 // Cooperative launch plan for B swarms of P particles: chunk size (the
 // throughput block, or with `latency` the 256-lane block when every swarm then
 // still gets its own CUs), G chunks per swarm, NG concurrent groups (a
-// multiple of 8 for the XCD-aware membership, one workgroup per CU, at most
+// multiple of 8 for the XCD-aware membership, kCoopBlocksPerCU workgroups per CU, at most
 // ceil8(B)).  False if infeasible.
 bool coop_plan(const ChainHost& ch, int mode, int P, int64_t B, bool latency, int* G, int* NG, int* block)
 {

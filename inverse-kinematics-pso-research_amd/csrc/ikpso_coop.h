@@ -161,12 +161,19 @@ __device__ __forceinline__ void coop_exchange(SwarmShared<Topo>& sh, CoopShared<
 // better than 3 (the extra live values cost the step more than the window saves:
 // profiles/r03b, r03c variant_timings).
 template <class Topo, int MODE, int TERMS, int BLOCK>
-constexpr int kCoopAhead = (kTipBackward<Topo, MODE, TERMS> && BLOCK != kCoopLatencyThreads && Topo::D > 30) ? 3 : 0;
+constexpr int kCoopAhead = (kTipBackward<Topo, MODE, TERMS> && Topo::D > 30) ? 3 : 0;
+// Waves per SIMD a cooperative build is compiled for: its own (BLOCK / 256)
+// times the workgroups that share a CU (the latency variant: 1, alone on its
+// CU).  The long chains' collider builds need more than 256 VGPRs: compiled for
+// one workgroup per CU, and launch_coop_block fits the groups to that.
+template <int D, int BLOCK, int TERMS>
+constexpr int kCoopMinWaves = (BLOCK >= 256 ? BLOCK / 256 : 1) *
+                              (BLOCK == kCoopThreads<D>() && !(TERMS & kTermColliders) ? kCoopBlocksPerCU<D>() : 1);
 
 // BLOCK: kCoopThreads<D>() (throughput: fill each CU), or kCoopLatencyThreads
 // for a few swarms (latency: one wave per SIMD on 4x more CUs).
 template <class Topo, int MODE, int TERMS, int BLOCK>
-__global__ void __launch_bounds__(BLOCK, (BLOCK >= 256 ? BLOCK / 256 : 1))
+__global__ void __launch_bounds__(BLOCK, (kCoopMinWaves<Topo::D, BLOCK, TERMS>))
     k_swarm_coop(const ChainConsts<Topo::J> cc, const SwarmIO io)
 {
     constexpr int J = Topo::J;
@@ -174,9 +181,10 @@ __global__ void __launch_bounds__(BLOCK, (BLOCK >= 256 ? BLOCK / 256 : 1))
     const int tid = threadIdx.x;
     const int P = io.P;
 
-    // local bests [d][lane]; padded to > 80 KiB so a CU never holds two
-    // workgroups (the launch geometry assumes one per CU)
-    constexpr int kPb = (D * BLOCK * 4 > 82 * 1024) ? D * BLOCK : 82 * 1024 / 4;
+    // local bests [d][lane]; a build that owns its CU is padded to > 80 KiB so a
+    // CU never holds two of its workgroups (the launch geometry assumes one)
+    constexpr bool kOwnCU = kCoopMinWaves<D, BLOCK, TERMS> == (BLOCK >= 256 ? BLOCK / 256 : 1);
+    constexpr int kPb = (!kOwnCU || D * BLOCK * 4 > 82 * 1024) ? D * BLOCK : 82 * 1024 / 4;
     __shared__ SwarmLds<Topo, kPb, CoopShared<J>> lds;
     SwarmShared<Topo>& sh = lds.sh;
     CoopShared<J>& cs = lds.extra;
@@ -204,7 +212,7 @@ __global__ void __launch_bounds__(BLOCK, (BLOCK >= 256 ? BLOCK / 256 : 1))
         stage_swarm_inputs<Topo, TERMS>(cc, io.targets, io.start_pose, b, sh);
         // the add-for-shift issue form only in the latency variant (one wave per
         // SIMD, room to spare): in the 2-wave serial-20 kernel it cost 5 %
-        using Rng = XorwowT<BLOCK == kCoopLatencyThreads && std::is_same_v<RngFor<TERMS>, XorwowT<true>>>;
+        using Rng = XorwowT<kOwnCU && BLOCK == kCoopLatencyThreads && std::is_same_v<RngFor<TERMS>, XorwowT<true>>>;
         Rng rng{0, 0, 0, 0, 0, 0};
         if (i < P) load_rng(rng, io.rng + b * P + i);
         if (tid == 0) cs.gkey = 0xFFFFFFFFu;
@@ -306,7 +314,7 @@ __global__ void __launch_bounds__(BLOCK, (BLOCK >= 256 ? BLOCK / 256 : 1))
     }
 }
 
-// Launch: grid = NG * G workgroups, at most one per CU.  Co-residency is
+// Launch: grid = NG * G workgroups, at most kCoopBlocksPerCU per CU.  Co-residency is
 // checked here against the occupancy query (the check hipLaunchCooperativeKernel
 // would make; a plain launch gives the same residency without the cooperative
 // queue): an oversized grid is an error, never a hang.
@@ -319,9 +327,18 @@ inline hipError_t launch_coop_block(const ChainConsts<Topo::J>& cc, const SwarmI
     if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, T, 0);
     if (e != hipSuccess) return e;
-    const int64_t grid = (int64_t)io.coop_ng * io.coop_g;
-    if (per_cu < 1 || grid > (int64_t)cus) return hipErrorCooperativeLaunchTooLarge;
-    hipLaunchKernelGGL(kernel, dim3((unsigned)grid), dim3(T), 0, stream, cc, io);
+    // The plan assumed kCoopBlocksPerCU workgroups per CU; a build whose registers
+    // admit fewer (the long chains' collider builds exceed 256 VGPRs) runs fewer
+    // concurrent groups -- the slots carved for the plan's NG cover them.
+    const int want_per_cu = kCoopMinWaves<Topo::D, T, TERMS> / (T >= 256 ? T / 256 : 1);
+    const int fit = per_cu < want_per_cu ? per_cu : want_per_cu;
+    if (fit < 1) return hipErrorCooperativeLaunchTooLarge;
+    SwarmIO run = io;
+    const int ng_fit = (int)(((int64_t)cus * fit / io.coop_g) & ~int64_t(7));
+    if (ng_fit < 8) return hipErrorCooperativeLaunchTooLarge;
+    if (run.coop_ng > ng_fit) run.coop_ng = ng_fit;
+    const int64_t grid = (int64_t)run.coop_ng * run.coop_g;
+    hipLaunchKernelGGL(kernel, dim3((unsigned)grid), dim3(T), 0, stream, cc, run);
     return hipGetLastError();
 }
 

@@ -96,13 +96,21 @@ __host__ __device__ constexpr int kResidentMaxThreads()
     return D <= 30 ? 1024 : 256;
 }
 
-// Threads per workgroup of the cooperative kernel: the resident kernel's 1024
-// for short chains; 512 (2 waves per SIMD, <= 256 VGPRs, 120 KiB of local bests
-// at D = 60) for long ones.  One workgroup per CU either way (LDS).
+// Threads per workgroup of the cooperative kernel, and its workgroups per CU:
+// the resident kernel's 1024 for short chains, one per CU; for long ones 256
+// lanes (one wave per SIMD, 60 KiB of local bests at D = 60) and TWO workgroups
+// per CU, each a chunk of a different swarm -- 2 waves per SIMD (<= 256 VGPRs)
+// as with one 512-lane chunk, but one swarm's argmin barrier and cross-CU
+// hand-off hide under the other swarm's step.
 template <int D>
 __host__ __device__ constexpr int kCoopThreads()
 {
-    return D <= 30 ? 1024 : 512;
+    return D <= 30 ? 1024 : 256;
+}
+template <int D>
+__host__ __device__ constexpr int kCoopBlocksPerCU()
+{
+    return D <= 30 ? 1 : 2;
 }
 
 #ifndef IKPSO_COOP_TIMING

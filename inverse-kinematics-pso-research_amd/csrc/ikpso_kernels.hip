@@ -128,8 +128,9 @@ hipError_t launch_coop(const ChainHost& ch, int mode, const SwarmIO& io, hipStre
     return ok ? err : hipErrorInvalidValue;
 }
 
-// One cooperative workgroup per CU: the kernel's LDS block is at least 82 KiB
-// (more than half of a CU's 160 KiB), whatever the topology.
+// Cooperative workgroups per CU: one for short chains (the kernel's LDS block is
+// at least 82 KiB, more than half of a CU's 160 KiB), two for long ones
+// (kCoopBlocksPerCU).
 bool coop_geometry(const ChainHost& ch, int mode, CoopGeometry* g)
 {
     (void)mode;
@@ -138,6 +139,7 @@ bool coop_geometry(const ChainHost& ch, int mode, CoopGeometry* g)
         using T = decltype(topo);
         if constexpr (!T::kGeneric) {
             g->threads = kCoopThreads<T::D>();
+            g->blocks_per_cu = kCoopBlocksPerCU<T::D>();
             g->latency_variant = kCoopThreads<T::D>() != kCoopLatencyThreads;
             spec = true;
         }
@@ -146,7 +148,6 @@ bool coop_geometry(const ChainHost& ch, int mode, CoopGeometry* g)
     int dev = 0, cus = 0;
     if (hipGetDevice(&dev) != hipSuccess) return false;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) return false;
-    g->blocks_per_cu = 1;
     g->cus = cus;
     return true;
 }

@@ -122,3 +122,26 @@ def _with_targets(chain, tg):
     ch = chain.copy()
     ch["target_position"][5:8] = tg
     return ch
+
+
+def test_long_chain_colliders_cooperative(oracle, device):
+    """A 12-joint serial chain (D = 36) with colliders solved by the cooperative
+    kernel: its collider build needs more than 256 VGPRs, so it cannot run the two
+    workgroups per CU the long-chain geometry plans; the launch fits the
+    concurrent groups to the build's real occupancy (one per CU) instead of
+    failing.  REFERENCE arithmetic: bit-exact to the oracle."""
+    chain = ikpso.serial_chain(12, length=0.4).to_cuda()
+    boxes = ikpso.init_colliders(2)
+    B, P, I = 3, 1024, 6
+    rng = np.random.default_rng(23)
+    tg = rng.uniform(-2.0, 2.0, (B, 1, 3)).astype(np.float32)
+    s = ikpso.BatchSolver(chain, P, pso=ikpso.PSOConfig(0.5, 0.5, 1.25, I), arith="reference", kernel="coop",
+                          colliders=boxes)
+    assert "coop" in s.kernel and "serial_tip12" in s.kernel
+    s.seed(B)
+    ang, fit, res = (t.cpu().numpy() for t in s.solve(dev(tg), iterations=I))
+    assert s.fallbacks == 0
+    s.close()
+    ostate = oracle.init_generators(B * P, 0)
+    oang, ofit, ores = oracle.solve_batch(chain, tg, None, P, I, ostate, colliders=boxes, threads=4)
+    assert np.array_equal(ang, oang) and np.array_equal(fit, ofit)

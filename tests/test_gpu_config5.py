@@ -1,9 +1,9 @@
 """BASELINE config 5 at its own configuration, against the CPU oracle.
 
 The benchmarked config-5 kernel is k_swarm_coop<TopoSerialTip<20>>: a swarm of
-4096 particles of the 20-joint chain (D = 60) over G = 8 co-resident 512-lane
-chunks (8 CUs), exchanging chunk minima through L2 every iteration, with the
-soft joint-limit penalty.  Reference semantics: calculatePSO,
+4096 particles of the 20-joint chain (D = 60) over G = 16 co-resident 256-lane
+chunks (two chunks of different swarms per CU), exchanging chunk minima through
+L2 every iteration, with the soft joint-limit penalty.  Reference semantics: calculatePSO,
 src/kernel.cu:279-327 (init, then I x update / evaluate / first-minimum argmin /
 strict global-best improvement); SURVEY.md §8(c) tiers A and B.
 
@@ -60,7 +60,7 @@ def oracle_batch(oracle, wl, B, I, threads=0):
 
 
 def test_config5_reference_bitexact_g8(oracle, device):
-    """2 swarms x 4096 particles x 20 iterations through k_swarm_coop with G = 8."""
+    """2 swarms x 4096 particles x 20 iterations through k_swarm_coop with G = 16."""
     B, I = 2, 20
     wl, s = config5_solver("reference", I)
     assert s.kernel == "swarm_coop<serial_tip20>", s.kernel

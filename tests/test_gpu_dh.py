@@ -58,7 +58,7 @@ def test_dh_solves_reachable_targets(device, spec):
     tg = reachable_targets(spec, B, rng)
     fit_cfg = ikpso.FitnessConfig(0.0, 0.0, 0.1)  # position only: no pull towards the rest pose
     s = ikpso.BatchSolver(chain, 1024, pso=ikpso.PSOConfig(0.5, 0.5, 1.25, 400), fit=fit_cfg)
-    # 7 nodes: one workgroup per swarm; 11 nodes (iiwa: 4 d offsets): two 512-lane chunks per swarm
+    # 7 nodes: one workgroup per swarm; 11 nodes (iiwa: 4 d offsets): four 256-lane chunks per swarm
     assert ("resident" if len(chain) == 8 else "coop") in s.kernel
     s.seed(B)
     ang, fit, res = (t.cpu().numpy() for t in s.solve(dev(tg.reshape(B, 1, 3)), iterations=400))

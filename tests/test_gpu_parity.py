@@ -198,18 +198,24 @@ def tier_b_case(oracle):
     return wl, tg, oang, ofit, ores, ostate
 
 
+@pytest.mark.parametrize("kernel", ["resident", "auto"])
 @pytest.mark.parametrize("arith", ["fast", "reference"])
-def test_tier_b_config3_batch(oracle, device, tier_b_case, arith):
+def test_tier_b_config3_batch(oracle, device, tier_b_case, arith, kernel):
     """Tier B: >= 90 % of the 64 swarms within |df|/f <= 1e-3 of the oracle's
     gbest fitness, mean gbest fitness within 0.5 %, mean residual within 1e-3 +
     1 %; the generator states after 500 iterations are bit-exact (draw count).
-    REFERENCE arithmetic: every swarm bit-exact."""
+    REFERENCE arithmetic: every swarm bit-exact.  AUTO with 64 swarms runs the
+    cooperative latency variant (4 CUs per swarm: config 2's kernel) over the
+    same 64 swarms of 1024 x 500."""
     wl, tg, oang, ofit, ores, ostate = tier_b_case
     B, P, I = TIER_B_SWARMS, wl.particles, wl.iterations
-    s = ikpso.BatchSolver(wl.chain, P, pso=wl.pso, arith=arith, kernel="resident")
+    s = ikpso.BatchSolver(wl.chain, P, pso=wl.pso, arith=arith, kernel=kernel)
     s.seed(B)
     ang, fit, res = (t.cpu().numpy() for t in s.solve(dev(tg), iterations=I))
+    assert ("latency variant" in s.kernel) == (kernel == "auto"), s.kernel
+    states = s.generator_states(0, B)
     s.close()
+    assert np.array_equal(states[:, :6], rng_words(ostate))
     if arith == "reference":
         assert np.array_equal(ang, oang) and np.array_equal(fit, ofit)
         return
@@ -460,7 +466,7 @@ def test_batch_streaming_equals_resident(device, batch_case):
 def test_config5_chain_with_penalty(oracle, device, arith, kernel):
     """BASELINE config 5 shape at test size: 20-joint serial chain (D = 60), tip
     effector, soft joint-limit penalty (extension); streaming and cooperative
-    kernels (P = 1024: two 512-lane chunks per swarm)."""
+    kernels (P = 1024: four 256-lane chunks per swarm)."""
     wl = ikpso.workload(5)
     B, P, I = 3, 1024, 10
     tg = wl.targets(0, B)
