@@ -555,7 +555,7 @@ hipError_t carve_coop(SwarmIO& io, void* ws, int G, int NG, int block, int D, hi
     Carver cv{static_cast<char*>(ws)};
     io.coop_error = cv.take<int32_t>(1);
     io.coop_slots = cv.take<unsigned long long>((size_t)NG * 2 * G * kCoopSlot(D));
-    io.coop_timing = IKPSO_COOP_TIMING ? cv.take<unsigned long long>((size_t)NG * G * 4) : nullptr;
+    io.coop_timing = IKPSO_COOP_TIMING ? cv.take<unsigned long long>((size_t)NG * G * 8) : nullptr;
     io.coop_g = G;
     io.coop_ng = NG;
     io.coop_block = block;
@@ -563,7 +563,7 @@ hipError_t carve_coop(SwarmIO& io, void* ws, int G, int NG, int block, int D, hi
     const size_t zero = reinterpret_cast<char*>(io.coop_slots + (size_t)NG * 2 * G * kCoopSlot(D)) -
                         static_cast<char*>(ws);
     if (IKPSO_COOP_TIMING) {
-        const hipError_t e = hipMemsetAsync(io.coop_timing, 0, (size_t)NG * G * 32, s);
+        const hipError_t e = hipMemsetAsync(io.coop_timing, 0, (size_t)NG * G * 64, s);
         if (e != hipSuccess) return e;
     }
     return hipMemsetAsync(ws, 0, zero, s);
@@ -1045,14 +1045,15 @@ ikpso_status ikpso_solver_sync(ikpso_solver* s)
     IKPSO_HIP(hipStreamSynchronize(p.stream));
 #if IKPSO_COOP_TIMING
     if (s->pending_timing) {  // measurement build: mean cycles per iteration over the workgroups
-        std::vector<unsigned long long> t((size_t)s->pending_timing_n * 4);
+        std::vector<unsigned long long> t((size_t)s->pending_timing_n * 8);
         IKPSO_HIP(hipMemcpy(t.data(), s->pending_timing, t.size() * 8, hipMemcpyDeviceToHost));
-        double a = 0, b = 0, c = 0, it = 0;
-        for (size_t i = 0; i < t.size(); i += 4) a += t[i], b += t[i + 1], it += t[i + 2], c += t[i + 3];
+        double a = 0, b = 0, c = 0, it = 0, imp = 0, rem = 0, pol = 0;
+        for (size_t i = 0; i < t.size(); i += 8)
+            a += t[i], b += t[i + 1], it += t[i + 2], c += t[i + 3], imp += t[i + 4], rem += t[i + 5], pol += t[i + 6];
         fprintf(stderr,
                 "ikpso coop timing: %d workgroups, per iteration (wave 0): step %.0f, argmin barrier %.0f, "
-                "hand-off %.0f cycles\n",
-                s->pending_timing_n, a / it, c / it, b / it);
+                "hand-off %.0f cycles; improving exchanges %.3f (won by another chunk %.3f), key polls %.2f\n",
+                s->pending_timing_n, a / it, c / it, b / it, imp / it, rem / it, pol / it);
     }
 #endif
     if (!err) return IKPSO_OK;

@@ -72,6 +72,7 @@ struct CoopShared {
     granule_t* slots;   // the group's [2][G] published records (kCoopSlot granules each)
 #if IKPSO_COOP_TIMING
     unsigned long long t_mid;  // wave 0 past the local argmin (timing builds)
+    unsigned int n_imp, n_remote, n_polls;  // improving exchanges, ... won by another chunk, key polls
 #endif
 };
 
@@ -119,11 +120,20 @@ __device__ __forceinline__ void coop_exchange(SwarmShared<Topo>& sh, CoopShared<
             }
             __builtin_amdgcn_s_sleep(1);
         }
+#if IKPSO_COOP_TIMING
+        if (lane == 0) cs.n_polls += n + 1;
+#endif
         const uint32_t k = lane < G ? (uint32_t)kg : 0xFFFFFFFFu;
         const uint32_t gmin = wave_min_u32(k);
         const int wj = wave_first_lane_eq(k, gmin);
         const uint32_t cur = cs.gkey;
         if (!timed_out && (force || gmin < cur)) {  // uniform within wave 0
+#if IKPSO_COOP_TIMING
+            if (lane == 0 && !force) {
+                cs.n_imp += 1;
+                cs.n_remote += wj != member;
+            }
+#endif
             float gv = mine_d;  // this chunk won: its own vector, no hop
             if (wj != member) {
                 granule_t vg;
@@ -199,6 +209,9 @@ __global__ void __launch_bounds__(BLOCK, (kCoopMinWaves<Topo::D, BLOCK, TERMS>))
         cs.e = 0;
         cs.abort = 0;
         cs.b = group;
+#if IKPSO_COOP_TIMING
+        cs.n_imp = cs.n_remote = cs.n_polls = 0;
+#endif
         cs.slots = io.coop_slots + (size_t)group * 2 * G * kCoopSlot(D);
     }
     __syncthreads();
@@ -210,9 +223,13 @@ __global__ void __launch_bounds__(BLOCK, (kCoopMinWaves<Topo::D, BLOCK, TERMS>))
         if (b >= io.num_swarms) break;
         const int i = cs.member * BLOCK + tid;  // particle index within the swarm
         stage_swarm_inputs<Topo, TERMS>(cc, io.targets, io.start_pose, b, sh);
-        // the add-for-shift issue form only in the latency variant (one wave per
-        // SIMD, room to spare): in the 2-wave serial-20 kernel it cost 5 %
-        using Rng = XorwowT<kOwnCU && BLOCK == kCoopLatencyThreads && std::is_same_v<RngFor<TERMS>, XorwowT<true>>>;
+        // the add-for-shift issue form (t + t for t << 1) in the latency variant
+        // (one wave per SIMD, room to spare) and in the long-chain build: 2 %
+        // faster on config 5's two-chunks-per-CU kernel (profiles/r03f
+        // variant_timings), where round 2's one-512-lane-chunk kernel had
+        // measured it 5 % slower; the short chains' 1024-lane cooperative build keeps the shift
+        using Rng = XorwowT<((kOwnCU && BLOCK == kCoopLatencyThreads) || D > 30) &&
+                            std::is_same_v<RngFor<TERMS>, XorwowT<true>>>;
         Rng rng{0, 0, 0, 0, 0, 0};
         if (i < P) load_rng(rng, io.rng + b * P + i);
         if (tid == 0) cs.gkey = 0xFFFFFFFFu;
@@ -263,11 +280,15 @@ __global__ void __launch_bounds__(BLOCK, (kCoopMinWaves<Topo::D, BLOCK, TERMS>))
         }
 #if IKPSO_COOP_TIMING
         if (tid == 0) {
-            unsigned long long* tm = io.coop_timing + (size_t)blockIdx.x * 4;
+            unsigned long long* tm = io.coop_timing + (size_t)blockIdx.x * 8;
             tm[0] += t_step;
             tm[1] += t_exch;
             tm[2] += n_it;
             tm[3] += t_bar;
+            tm[4] += cs.n_imp;
+            tm[5] += cs.n_remote;
+            tm[6] += cs.n_polls;
+            cs.n_imp = cs.n_remote = cs.n_polls = 0;
         }
 #endif
 

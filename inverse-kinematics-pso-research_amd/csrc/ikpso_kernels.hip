@@ -155,7 +155,7 @@ bool coop_geometry(const ChainHost& ch, int mode, CoopGeometry* g)
 size_t coop_workspace_bytes(int ng, int G, int D, int block)
 {
     return 8 * (size_t)ng * 2 * G * kCoopSlot(D) +
-           256 + 3 * 256 + (IKPSO_COOP_TIMING ? 32 * (size_t)ng * G + 256 : 0);
+           256 + 3 * 256 + (IKPSO_COOP_TIMING ? 64 * (size_t)ng * G + 256 : 0);
 }
 
 hipError_t launch_stream(const ChainHost& ch, int mode, const StreamIO& io, int iterations, hipStream_t stream)
