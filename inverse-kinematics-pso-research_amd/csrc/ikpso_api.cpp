@@ -905,7 +905,9 @@ ikpso_status ikpso_solver_create(const ikpso_solver_desc* desc, ikpso_solver** o
     s->family = pick_kernel(sch, s->mode, s->P, desc->kernel);
     s->requested = desc->kernel;
     if (s->family >= 0) s->kname = kernel_name(sch, s->family);
-    if (s->family >= 0) s->kname_latency = kernel_name(sch, IKPSO_KERNEL_COOP) + " (latency variant)";
+    if (s->family >= 0)
+        s->kname_latency = kernel_name(sch, IKPSO_KERNEL_COOP) +
+                           (coop_latency_split(sch) ? " (latency variant, generator waves)" : " (latency variant)");
     if (s->family < 0 || desc->kernel < IKPSO_KERNEL_AUTO || desc->kernel > IKPSO_KERNEL_COOP) {
         (void)hipFree(s->aux);
         if (s->aux_dh) (void)hipFree(s->aux_dh);

@@ -363,12 +363,268 @@ inline hipError_t launch_coop_block(const ChainConsts<Topo::J>& cc, const SwarmI
     return hipGetLastError();
 }
 
+// ------------------------------------------------ latency variant, generator split
+// A swarm spread thin (config 2: 1024 particles over 4 CUs, one wave per SIMD)
+// is bound by ONE wave's instruction stream per iteration: a lone wave issues at
+// most every 4 cycles (8 for the half-rate and transcendental forms), so the
+// step takes ~5 900 cycles for 1 079 instructions (IKPSO_COOP_TIMING,
+// profiles/r03f/variant_timings/var_r7_latency.txt) while three of a SIMD's
+// four issue slots stay empty.  More than half of those instructions are the
+// XORWOW generator, which depends on nothing but its own state.  Here each
+// 256-particle chunk gets 512 lanes: waves 0-3 compute (update, FK, fitness,
+// local bests, exchange) and waves 4-7 run the generators of the same 256
+// particles one iteration ahead, writing each draw converted to float
+// (v_cvt_f32_u32 of the XORWOW output, exactly what uniform()/scaled() start
+// from) into an LDS block [quad][lane][4]; the compute lanes read four draws per
+// ds_read_b128 and finish them with the one FMA of uniform()/scaled().  The draw
+// order, the values and the final generator states are the unsplit kernel's,
+// bit for bit, in both arithmetic modes.  Block m (0: the D init draws, m >= 1:
+// the 3D draws of iteration m - 1) lives in buffer m & 1; the generator waves
+// produce block m while iteration m - 2 runs -- quads [0, QA) beside the compute
+// waves' step, the rest while wave 0 hands the chunk's minimum off -- so the two
+// buffers alternate behind the exchange's barriers.  LDS: 2 x 64 KiB of draw
+// blocks + 21 KiB of local bests at D = 21, so D <= 21; masked chains (their draw
+// count is a runtime mask) and collider builds keep the unsplit latency kernel.
+template <class Topo, int TERMS>
+constexpr bool kSplitGen = IKPSO_SPLIT_GEN && Topo::D <= 21 && !kMasked<Topo, TERMS> && !(TERMS & kTermColliders);
+template <int D>
+constexpr int kSplitQuads = (3 * D + 3) / 4;  // float4 quads of the largest block (an iteration's 3D draws)
+// quads of an iteration block the generator waves write beside the step (the rest during the hand-off)
+template <int D>
+constexpr int kSplitQA = IKPSO_SPLIT_QA < 0 ? kSplitQuads<D> / 2 : (IKPSO_SPLIT_QA < kSplitQuads<D> ? IKPSO_SPLIT_QA : kSplitQuads<D>);
+
+// The compute lanes' draw source: the interface of XorwowT (uniform(), scaled())
+// over one lane's column of an LDS block.  Fully unrolled callers make k a
+// constant at every call site, so each quad is one ds_read_b128 at an immediate offset.
+template <int BC>
+struct LdsDraws {
+    const float4* p;  // the lane's column: p[q * BC] holds draws 4q .. 4q + 3
+    int k;
+    float4 cur;
+    __device__ __forceinline__ float raw()
+    {
+        if ((k & 3) == 0) cur = p[(k >> 2) * BC];
+        const int c = k & 3;
+        ++k;
+        return c == 0 ? cur.x : c == 1 ? cur.y : c == 2 ? cur.z : cur.w;
+    }
+    __device__ __forceinline__ float uniform() { return __builtin_fmaf(raw(), 2.3283064e-10f, 1.16415322e-10f); }
+    __device__ __forceinline__ float scaled(float q, float h) { return __builtin_fmaf(raw(), q, h); }
+};
+
+// Generator lanes: quads [Q0, Q1) of a block of N draws into the lane's column.
+template <int N, int Q0, int Q1, int BC, class Rng>
+__device__ __forceinline__ void gen_quads(Rng& rng, float4* col)
+{
+#pragma unroll
+    for (int q = Q0; q < Q1; ++q) {
+        float f[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) f[c] = 4 * q + c < N ? (float)rng.next() : 0.0f;
+        col[q * BC] = make_float4(f[0], f[1], f[2], f[3]);
+    }
+}
+
+template <class Topo, int BC>
+struct SplitLds {
+    static constexpr int D = Topo::D, NQ = kSplitQuads<Topo::D>;
+    SwarmShared<Topo> sh;
+    CoopShared<Topo::J> cs;
+    float pb[D * BC];            // local bests [d][lane]
+    float4 draws[2][NQ * BC];    // draw blocks [buffer][quad][lane]
+    // more than half of a CU's LDS: one workgroup per CU (the launch plan's geometry)
+    char pad[(int)sizeof(SwarmShared<Topo>) + D * BC * 4 + 2 * NQ * BC * 16 > 82 * 1024
+                 ? 1
+                 : 82 * 1024 - (int)sizeof(SwarmShared<Topo>) - D * BC * 4 - 2 * NQ * BC * 16];
+};
+
+template <class Topo, int MODE, int TERMS>
+__global__ void __launch_bounds__(2 * kCoopLatencyThreads) k_swarm_coop_split(const ChainConsts<Topo::J> cc,
+                                                                               const SwarmIO io)
+{
+    constexpr int D = Topo::D;
+    constexpr int BC = kCoopLatencyThreads;  // particles per chunk = compute lanes = generator lanes
+    constexpr int NQ = kSplitQuads<D>, QA = kSplitQA<D>;
+    constexpr int NQI = (D + 3) / 4;  // quads of the init block
+    __shared__ SplitLds<Topo, BC> lds;
+    SwarmShared<Topo>& sh = lds.sh;
+    CoopShared<Topo::J>& cs = lds.cs;
+    float* const s_pb = lds.pb;
+    const int tid = threadIdx.x;
+    const bool gen = wave_id() >= BC / 64;  // uniform per wave
+    const int lc = gen ? tid - BC : tid;    // the particle (within the chunk) this lane serves
+    const int P = io.P;
+    if (tid == 0) {
+        const int G = io.coop_g;
+        const int xcd = blockIdx.x & 7, pos = blockIdx.x >> 3;
+        const int group = (pos / G) * 8 + xcd;
+        cs.G = G;
+        cs.member = pos % G;
+        cs.e = 0;
+        cs.abort = 0;
+        cs.b = group;
+#if IKPSO_COOP_TIMING
+        cs.n_imp = cs.n_remote = cs.n_polls = 0;
+#endif
+        cs.slots = io.coop_slots + (size_t)group * 2 * G * kCoopSlot(D);
+    }
+    __syncthreads();
+    const PsoCoef coef = pso_coef(cc);
+
+    for (;;) {
+        compiler_fence();
+        const int64_t b = cs.b;
+        if (b >= io.num_swarms) break;
+        const int i = cs.member * BC + lc;
+        stage_swarm_inputs<Topo, TERMS>(cc, io.targets, io.start_pose, b, sh);
+        using Rng = XorwowT<std::is_same_v<RngFor<TERMS>, XorwowT<true>>>;  // add-for-shift: see k_swarm_coop
+        Rng rng{0, 0, 0, 0, 0, 0};
+        const int I = io.iterations;
+        if (gen) {
+            if (i < P) load_rng(rng, io.rng + b * P + i);
+            gen_quads<D, 0, NQI, BC>(rng, lds.draws[0] + lc);  // block 0: initParticlesKernel's draws
+        }
+        if (tid == 0) cs.gkey = 0xFFFFFFFFu;
+        __syncthreads();
+
+        float x[D], v[D], pbf = 0.0f;
+#pragma unroll
+        for (int d = 0; d < D; ++d) x[d] = v[d] = 0.0f;
+        if (!gen) {
+            LdsDraws<BC> rd{lds.draws[0] + lc, 0, {}};
+            init_particle<Topo, TERMS, BC>(cc, sh, s_pb, lc, x, v, rd);
+            pbf = fitness<Topo, MODE, TERMS>(cc, x, sh.rest, sh.tgt, nullptr, sh.dh, sh.soft);
+        } else if (I > 0) {
+            gen_quads<3 * D, 0, QA, BC>(rng, lds.draws[1] + lc);
+        }
+        // the rest of block m + 2 (into buffer m & 1) while wave 0 hands off
+        int nb = 1;  // the block the generator waves are producing
+        auto ahead = [&]() {
+            if (gen) gen_quads<3 * D, QA, NQ, BC>(rng, lds.draws[nb & 1] + lc);
+        };
+        const uint32_t key0 = !gen && i < P ? ordered_key(pbf) : 0xFFFFFFFFu;
+        coop_exchange<Topo, BC>(sh, cs, s_pb, key0, io.coop_error, io.coop_spin_limit, true, I > 0, ahead);
+
+#if IKPSO_COOP_TIMING
+        unsigned long long t_step = 0, t_bar = 0, t_exch = 0, n_it = 0;
+#endif
+        for (int it = 0; it < I; ++it) {
+            compiler_fence();
+            if (cs.abort) break;
+#if IKPSO_COOP_TIMING
+            const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+#endif
+            nb = it + 2;
+            if (!gen) {
+                LdsDraws<BC> rd{lds.draws[(it + 1) & 1] + lc, 0, {}};
+                swarm_step<Topo, MODE, TERMS, BC>(cc, sh, s_pb, lc, x, v, pbf, coef, rd);
+            } else if (nb <= I) {
+                gen_quads<3 * D, 0, QA, BC>(rng, lds.draws[nb & 1] + lc);
+            }
+            const uint32_t key = !gen && i < P ? ordered_key(pbf) : 0xFFFFFFFFu;
+#if IKPSO_COOP_TIMING
+            const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+#endif
+            coop_exchange<Topo, BC>(sh, cs, s_pb, key, io.coop_error, io.coop_spin_limit, false, nb <= I, ahead);
+#if IKPSO_COOP_TIMING
+            const unsigned long long t2 = __builtin_amdgcn_s_memtime();
+            t_step += t1 - t0;
+            t_bar += cs.t_mid - t1;
+            t_exch += t2 - cs.t_mid;
+            ++n_it;
+#endif
+        }
+#if IKPSO_COOP_TIMING
+        if (tid == 0) {
+            unsigned long long* tm = io.coop_timing + (size_t)blockIdx.x * 8;
+            tm[0] += t_step;
+            tm[1] += t_exch;
+            tm[2] += n_it;
+            tm[3] += t_bar;
+            tm[4] += cs.n_imp;
+            tm[5] += cs.n_remote;
+            tm[6] += cs.n_polls;
+            cs.n_imp = cs.n_remote = cs.n_polls = 0;
+        }
+#endif
+
+        compiler_fence();
+        const int member = cs.member;
+        const int64_t bb = cs.b;
+        const int ii = member * BC + lc;
+        if (!gen && member == 0) {  // outputs (updateGlobalBestCoordsKernel) + fitness + residual
+            store_angles<Topo, TERMS>(cc, io.out_angles, bb, tid, tid < D ? sh.g[tid] : 0.0f);
+            if (tid == 0 && io.out_fitness) io.out_fitness[bb] = key_to_float(cs.gkey);
+            if (io.out_residual && tid < 64) {
+                float g[D];
+#pragma unroll
+                for (int d = 0; d < D; ++d) g[d] = sh.g[d];
+                const float r = residual<Topo, MODE, TERMS>(cc, g, sh.tgt, sh.dh);
+                if (tid == 0) io.out_residual[bb] = r;
+            }
+        }
+        if (ii < P) {
+            if (gen) {
+                store_rng(rng, io.rng + bb * P + ii);
+            } else {
+                if (io.dump_particles) {  // reference particles layout [3][D][P] per swarm
+                    float* base = io.dump_particles + bb * (int64_t)3 * D * P;
+#pragma unroll
+                    for (int d = 0; d < D; ++d) {
+                        base[(int64_t)d * P + ii] = radians<TERMS>(x[d]);
+                        base[(int64_t)(D + d) * P + ii] = radians<TERMS>(v[d]);
+                        base[(int64_t)(2 * D + d) * P + ii] = radians<TERMS>(s_pb[d * BC + lc]);
+                    }
+                }
+                if (io.dump_bests) io.dump_bests[bb * P + ii] = pbf;
+            }
+        }
+        __syncthreads();  // sh / s_pb / the draw blocks are reused by the next swarm; every wave has read cs
+        if (cs.abort) {
+            if (member == 0 && !gen)
+                for (int64_t r = bb; r < io.num_swarms; r += io.coop_ng) {
+                    if (tid < cc.dfree) io.out_angles[r * cc.dfree + tid] = __builtin_nanf("");
+                    if (tid == 0 && io.out_fitness) io.out_fitness[r] = __builtin_nanf("");
+                    if (tid == 0 && io.out_residual) io.out_residual[r] = __builtin_nanf("");
+                }
+            break;
+        }
+        if (tid == 0) cs.b = bb + io.coop_ng;
+        __syncthreads();
+    }
+}
+
+// One workgroup of 2 x kCoopLatencyThreads lanes per CU (the latency plan's geometry).
+template <class Topo, int MODE, int TERMS>
+inline hipError_t launch_coop_split(const ChainConsts<Topo::J>& cc, const SwarmIO& io, hipStream_t stream)
+{
+    const auto kernel = &k_swarm_coop_split<Topo, MODE, TERMS>;
+    constexpr int T = 2 * kCoopLatencyThreads;
+    int dev = 0, cus = 0, per_cu = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, T, 0);
+    if (e != hipSuccess) return e;
+    if (per_cu < 1) return hipErrorCooperativeLaunchTooLarge;
+    SwarmIO run = io;
+    const int ng_fit = (int)(((int64_t)cus / io.coop_g) & ~int64_t(7));
+    if (ng_fit < 8) return hipErrorCooperativeLaunchTooLarge;
+    if (run.coop_ng > ng_fit) run.coop_ng = ng_fit;
+    const int64_t grid = (int64_t)run.coop_ng * run.coop_g;
+    hipLaunchKernelGGL(kernel, dim3((unsigned)grid), dim3(T), 0, stream, cc, run);
+    return hipGetLastError();
+}
+
 template <class Topo, int MODE, int TERMS>
 inline hipError_t launch_coop_kernel(const ChainConsts<Topo::J>& cc, const SwarmIO& io, hipStream_t stream)
 {
     if constexpr (kCoopThreads<Topo::D>() != kCoopLatencyThreads) {
-        if (io.coop_block == kCoopLatencyThreads)
-            return launch_coop_block<Topo, MODE, TERMS, kCoopLatencyThreads>(cc, io, stream);
+        if (io.coop_block == kCoopLatencyThreads) {
+            if constexpr (kSplitGen<Topo, TERMS>)
+                return launch_coop_split<Topo, MODE, TERMS>(cc, io, stream);
+            else
+                return launch_coop_block<Topo, MODE, TERMS, kCoopLatencyThreads>(cc, io, stream);
+        }
     }
     if (io.coop_block != kCoopThreads<Topo::D>()) return hipErrorInvalidValue;
     return launch_coop_block<Topo, MODE, TERMS, kCoopThreads<Topo::D>()>(cc, io, stream);

@@ -116,6 +116,16 @@ __host__ __device__ constexpr int kCoopBlocksPerCU()
 #ifndef IKPSO_COOP_TIMING
 #define IKPSO_COOP_TIMING 0  // measurement builds: per-workgroup cycles in the step and in the hand-off
 #endif
+// The cooperative latency variant with its generators on separate waves
+// (k_swarm_coop_split, ikpso_coop.h); 0 builds the unsplit one (A/B timing).
+#ifndef IKPSO_SPLIT_GEN
+#define IKPSO_SPLIT_GEN 1
+#endif
+// Quads of an iteration's draw block the generator waves write beside the step
+// (the rest during the hand-off); -1: half.
+#ifndef IKPSO_SPLIT_QA
+#define IKPSO_SPLIT_QA -1
+#endif
 
 // Published record of one chunk, in 8-byte granules {value, tag}: the key, then
 // the D floats of the chunk winner's local best; padded to a 128-B multiple.
@@ -193,6 +203,7 @@ struct CoopGeometry {
 };
 bool coop_geometry(const ChainHost& ch, int mode, CoopGeometry* g);
 size_t coop_workspace_bytes(int ng, int G, int D, int block);
+bool coop_latency_split(const ChainHost& ch);  // latency variant with generator waves
 int resident_max_threads(const ChainHost& ch);
 bool chain_supported(const ChainHost& ch);
 std::string kernel_name(const ChainHost& ch, int family);  // IKPSO_KERNEL_*

@@ -152,6 +152,19 @@ bool coop_geometry(const ChainHost& ch, int mode, CoopGeometry* g)
     return true;
 }
 
+// The latency variant of this chain runs with its generators on separate waves
+// (k_swarm_coop_split: D <= 21, no mask, no collider block, hardware sin/cos range).
+bool coop_latency_split(const ChainHost& ch)
+{
+    bool split = false;
+    visit_topology(ch, [&](auto topo) {
+        using T = decltype(topo);
+        if constexpr (!T::kGeneric && kCoopThreads<T::D>() != kCoopLatencyThreads)
+            split = IKPSO_SPLIT_GEN && T::D <= 21 && (T::kDH || !ch.masked) && ch.num_coll == 0 && !ch.poly_trig;
+    });
+    return split;
+}
+
 size_t coop_workspace_bytes(int ng, int G, int D, int block)
 {
     return 8 * (size_t)ng * 2 * G * kCoopSlot(D) +

@@ -89,7 +89,7 @@ def test_auto_reports_latency_variant(device):
     assert s.kernel == "swarm_resident<ref_tree7>"
     s.seed(512)
     s.solve(dev(wl.targets(0, 1)), iterations=5)
-    assert s.kernel == "swarm_coop<ref_tree7> (latency variant)"
+    assert s.kernel == "swarm_coop<ref_tree7> (latency variant, generator waves)"
     s.solve(dev(wl.targets(0, 512)), iterations=5)
     assert s.kernel == "swarm_resident<ref_tree7>"
     s.close()
