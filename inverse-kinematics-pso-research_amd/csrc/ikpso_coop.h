@@ -393,11 +393,16 @@ constexpr int kSplitQuads = (3 * D + 3) / 4;  // float4 quads of the largest blo
 template <int D>
 constexpr int kSplitQA = IKPSO_SPLIT_QA < 0 ? kSplitQuads<D> / 2 : (IKPSO_SPLIT_QA < kSplitQuads<D> ? IKPSO_SPLIT_QA : kSplitQuads<D>);
 
-// The compute lanes' draw source: the interface of XorwowT (uniform(), scaled())
-// over one lane's column of an LDS block.  Fully unrolled callers make k a
-// constant at every call site, so each quad is one ds_read_b128 at an immediate offset.
-template <int BC>
+// The compute lanes' draw source: the interface of XorwowT over one lane's
+// column of an LDS block.  Fully unrolled callers make k a constant at every
+// call site, so each quad is one ds_read_b128 at an immediate offset.
+// PRE (iteration blocks): each draw already carries its PSO coefficient --
+// c * uniform() as pso_update forms it -- so scaled() and the REFERENCE
+// update's products take it as it is (kPrescaled); the init block holds
+// (float)next() for uniform().
+template <int BC, bool PRE>
 struct LdsDraws {
+    static constexpr bool kPrescaled = PRE;
     const float4* p;  // the lane's column: p[q * BC] holds draws 4q .. 4q + 3
     int k;
     float4 cur;
@@ -409,18 +414,46 @@ struct LdsDraws {
         return c == 0 ? cur.x : c == 1 ? cur.y : c == 2 ? cur.z : cur.w;
     }
     __device__ __forceinline__ float uniform() { return __builtin_fmaf(raw(), 2.3283064e-10f, 1.16415322e-10f); }
-    __device__ __forceinline__ float scaled(float q, float h) { return __builtin_fmaf(raw(), q, h); }
+    __device__ __forceinline__ float scaled(float q, float h)
+    {
+        if constexpr (PRE)
+            return raw();
+        else
+            return __builtin_fmaf(raw(), q, h);
+    }
 };
 
 // Generator lanes: quads [Q0, Q1) of a block of N draws into the lane's column.
-template <int N, int Q0, int Q1, int BC, class Rng>
-__device__ __forceinline__ void gen_quads(Rng& rng, float4* col)
+// Init block (MODE < 0): (float)next().  Iteration blocks: draw j is r1, r2 or r3
+// (j % 3) of its dimension, stored times its coefficient exactly as pso_update
+// forms it -- FAST fma((float)next(), c * 2^-32, c * 2^-33) (scaled()), REFERENCE
+// c * uniform() (the reference's first product, k.w * r1, ...).
+template <int N, int Q0, int Q1, int BC, int MODE, class Rng>
+__device__ __forceinline__ void gen_quads(Rng& rng, float4* col, const PsoCoef& k)
 {
 #pragma unroll
     for (int q = Q0; q < Q1; ++q) {
         float f[4];
 #pragma unroll
-        for (int c = 0; c < 4; ++c) f[c] = 4 * q + c < N ? (float)rng.next() : 0.0f;
+        for (int c = 0; c < 4; ++c) {
+            const int j = 4 * q + c;
+            if (j >= N) {
+                f[c] = 0.0f;
+            } else if constexpr (MODE < 0) {
+                f[c] = (float)rng.next();
+            } else if constexpr (MODE == IKPSO_ARITH_FAST) {
+                const float qq = j % 3 == 0 ? k.wq : j % 3 == 1 ? k.c1q : k.c2q;
+                const float hh = j % 3 == 0 ? k.wh : j % 3 == 1 ? k.c1h : k.c2h;
+                f[c] = rng.scaled(qq, hh);
+            } else {
+                const float cc = j % 3 == 0 ? k.w : j % 3 == 1 ? k.c1 : k.c2;
+                const float r = rng.uniform();
+                {
+#pragma clang fp contract(off)
+                    f[c] = cc * r;
+                }
+            }
+        }
         col[q * BC] = make_float4(f[0], f[1], f[2], f[3]);
     }
 }
@@ -482,7 +515,7 @@ __global__ void __launch_bounds__(2 * kCoopLatencyThreads) k_swarm_coop_split(co
         const int I = io.iterations;
         if (gen) {
             if (i < P) load_rng(rng, io.rng + b * P + i);
-            gen_quads<D, 0, NQI, BC>(rng, lds.draws[0] + lc);  // block 0: initParticlesKernel's draws
+            gen_quads<D, 0, NQI, BC, -1>(rng, lds.draws[0] + lc, coef);  // block 0: initParticlesKernel's draws
         }
         if (tid == 0) cs.gkey = 0xFFFFFFFFu;
         __syncthreads();
@@ -491,16 +524,16 @@ __global__ void __launch_bounds__(2 * kCoopLatencyThreads) k_swarm_coop_split(co
 #pragma unroll
         for (int d = 0; d < D; ++d) x[d] = v[d] = 0.0f;
         if (!gen) {
-            LdsDraws<BC> rd{lds.draws[0] + lc, 0, {}};
+            LdsDraws<BC, false> rd{lds.draws[0] + lc, 0, {}};
             init_particle<Topo, TERMS, BC>(cc, sh, s_pb, lc, x, v, rd);
             pbf = fitness<Topo, MODE, TERMS>(cc, x, sh.rest, sh.tgt, nullptr, sh.dh, sh.soft);
         } else if (I > 0) {
-            gen_quads<3 * D, 0, QA, BC>(rng, lds.draws[1] + lc);
+            gen_quads<3 * D, 0, QA, BC, MODE>(rng, lds.draws[1] + lc, coef);
         }
         // the rest of block m + 2 (into buffer m & 1) while wave 0 hands off
         int nb = 1;  // the block the generator waves are producing
         auto ahead = [&]() {
-            if (gen) gen_quads<3 * D, QA, NQ, BC>(rng, lds.draws[nb & 1] + lc);
+            if (gen) gen_quads<3 * D, QA, NQ, BC, MODE>(rng, lds.draws[nb & 1] + lc, coef);
         };
         const uint32_t key0 = !gen && i < P ? ordered_key(pbf) : 0xFFFFFFFFu;
         coop_exchange<Topo, BC>(sh, cs, s_pb, key0, io.coop_error, io.coop_spin_limit, true, I > 0, ahead);
@@ -516,10 +549,10 @@ __global__ void __launch_bounds__(2 * kCoopLatencyThreads) k_swarm_coop_split(co
 #endif
             nb = it + 2;
             if (!gen) {
-                LdsDraws<BC> rd{lds.draws[(it + 1) & 1] + lc, 0, {}};
+                LdsDraws<BC, true> rd{lds.draws[(it + 1) & 1] + lc, 0, {}};
                 swarm_step<Topo, MODE, TERMS, BC>(cc, sh, s_pb, lc, x, v, pbf, coef, rd);
             } else if (nb <= I) {
-                gen_quads<3 * D, 0, QA, BC>(rng, lds.draws[nb & 1] + lc);
+                gen_quads<3 * D, 0, QA, BC, MODE>(rng, lds.draws[nb & 1] + lc, coef);
             }
             const uint32_t key = !gen && i < P ? ordered_key(pbf) : 0xFFFFFFFFu;
 #if IKPSO_COOP_TIMING

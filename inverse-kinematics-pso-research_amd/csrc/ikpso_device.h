@@ -1082,10 +1082,27 @@ __device__ __forceinline__ PsoCoef pso_coef(const CC& cc)
 // coefficient into its uniform's affine map, c*r = c*(u*2^-32 + 2^-33) =
 // fma(u, c*2^-32, c*2^-33): one rounding where the reference has two (and
 // three fewer multiplies per dimension).
+// A draw source whose draws already carry their coefficient (the iteration
+// blocks of the generator-split kernel, LdsDraws) sets kPrescaled.
+template <class Rng, class = void>
+struct Prescaled : std::false_type {};
+template <class Rng>
+struct Prescaled<Rng, std::void_t<decltype(Rng::kPrescaled)>> : std::bool_constant<Rng::kPrescaled> {};
+
 template <int MODE, class Rng>
 __device__ __forceinline__ void pso_update(float& x, float& v, float pb, float g, const PsoCoef& k, Rng& rng)
 {
-    if constexpr (MODE == IKPSO_ARITH_REFERENCE) {
+    if constexpr (MODE == IKPSO_ARITH_REFERENCE && Prescaled<Rng>::value) {
+        // the same operations with the first products (w * r1, c1 * r2, c2 * r3) drawn
+        const float wr1 = rng.raw();
+        const float c1r2 = rng.raw();
+        const float c2r3 = rng.raw();
+        {
+#pragma clang fp contract(off)
+            v = wr1 * v + c1r2 * (pb - x) + c2r3 * (g - x);
+            x += v;
+        }
+    } else if constexpr (MODE == IKPSO_ARITH_REFERENCE) {
         const float r1 = rng.uniform();
         const float r2 = rng.uniform();
         const float r3 = rng.uniform();

@@ -30,12 +30,16 @@ def reachable_targets(arm_spec, n, rng):
     return np.array([dh_forward(t, arm_spec["d"], arm_spec["a"], arm_spec["alpha"]) for t in th], np.float32)
 
 
-@pytest.mark.parametrize("spec,kern", [(IIWA, "serial_tip11"), (PLANARISH, "serial_tip7")])
-def test_dh_reference_bitexact(oracle, device, spec, kern):
+@pytest.mark.parametrize("spec,kern,P", [(IIWA, "serial_tip11", 256), (PLANARISH, "serial_tip7", 256),
+                                         (PLANARISH, "serial_tip7", 1024)])
+def test_dh_reference_bitexact(oracle, device, spec, kern, P):
+    """REFERENCE, bit-exact to the oracle.  The 7-joint arm's swarms take the
+    cooperative latency variant with generator waves: one chunk at P = 256, four
+    at P = 1024."""
     arm = dh_arm(spec["a"], spec["alpha"], spec["d"], -LIM, LIM)
     chain = arm.origin.to_cuda()
     rng = np.random.default_rng(5)
-    B, P, I = 4, 256, 12
+    B, I = 4, 12
     tg = reachable_targets(spec, B, rng).reshape(B, 1, 3)
     s = ikpso.BatchSolver(chain, P, pso=ikpso.PSOConfig(0.5, 0.5, 1.25, I), arith="reference")
     assert kern in s.kernel
