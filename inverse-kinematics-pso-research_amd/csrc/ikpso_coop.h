@@ -105,14 +105,28 @@ __device__ __forceinline__ void coop_exchange(SwarmShared<Topo>& sh, CoopShared<
         granule_t* base = cs.slots + (size_t)(e & 1) * G * SLOT;
         // granule 0: the key; granules 1..D: the chunk winner's local best
         const float mine_d = lane >= 1 && lane <= D ? s_pb[(lane - 1) * BLOCK + lidx] : 0.0f;
+        // Short chains (kPollFirst): the other chunks' key granules are requested BEFORE
+        // this chunk's record is stored (its own key is known), so the first poll's
+        // wait does not include the store's write-through (vmcnt counts stores).
+        // Every lane loads -- lanes past G re-read chunk 0's key -- so no lane's branch
+        // has to wait for the load before the store issues.  Config 2: 1.394 -> 1.342
+        // ms; config 5 (D = 60): no gain (61.3 vs 61.5 ms), so not there
+        // (profiles/r03m/variant_timings/var_*_pf.txt).
+        constexpr bool kPollFirst = D <= 30;
+        granule_t kraw = kPollFirst ? ld_granule(base + (size_t)(lane < G ? lane : 0) * SLOT) : tag;
         if (lane <= D) st_granule(base + (size_t)member * SLOT + lane, tag | (lane == 0 ? lmin : __float_as_uint(mine_d)));
         if (do_ahead) ahead();
         // the G key granules, in chunk order (lanes 0..G-1; G <= 64)
         uint32_t n = 0;
         int timed_out = 0;
         granule_t kg;
-        for (;;) {
-            kg = lane < G ? ld_granule(base + (size_t)lane * SLOT) : tag;
+        for (int first = 1;; first = 0) {
+            if constexpr (kPollFirst) {
+                if (!first) kraw = ld_granule(base + (size_t)(lane < G ? lane : 0) * SLOT);
+                kg = lane == member ? (tag | lmin) : lane < G ? kraw : tag;
+            } else {
+                kg = lane < G ? ld_granule(base + (size_t)lane * SLOT) : tag;
+            }
             if (__builtin_amdgcn_ballot_w64((kg >> 32) != (granule_t)(e + 1)) == 0) break;
             if (spin_limit == 0 || n++ >= spin_limit) {  // spin_limit 0 (IKPSO_COOP_SPIN_LIMIT=0): the give-up path
                 timed_out = 1;
