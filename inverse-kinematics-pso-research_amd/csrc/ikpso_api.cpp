@@ -116,9 +116,20 @@ uint32_t as_bits(float f)
 }
 
 // Copy `bytes` from host, managed or device memory into host memory.
+// Host copy of a caller buffer in any memory: plain or pinned host memory is
+// copied on the CPU (the visualiser's per-frame call passes its node table every
+// frame: a hipMemcpy would cost a device round trip); device and managed memory
+// through hipMemcpy, which also orders it after the caller's GPU work.
 ikpso_status fetch_any(void* dst, const void* src, size_t bytes)
 {
     if (bytes == 0) return IKPSO_OK;
+    hipPointerAttribute_t a{};
+    const hipError_t e = hipPointerGetAttributes(&a, src);
+    if (e != hipSuccess) (void)hipGetLastError();  // an unregistered host pointer may report an error
+    if (e != hipSuccess || a.type == hipMemoryTypeUnregistered || a.type == hipMemoryTypeHost) {
+        memcpy(dst, src, bytes);
+        return IKPSO_OK;
+    }
     IKPSO_HIP(hipMemcpy(dst, src, bytes, hipMemcpyDefault));
     return IKPSO_OK;
 }
@@ -439,6 +450,7 @@ bool build_dh(const std::vector<ikpso_node>& nodes, const ChainHost& eu, const E
 std::mutex g_scratch_mu;
 float* g_scratch = nullptr;
 size_t g_scratch_bytes = 0;
+int32_t* g_err_pinned = nullptr;  // the cooperative error flag's host copy (pinned)
 
 ikpso_status scratch(size_t bytes, float** out)
 {
@@ -791,10 +803,15 @@ ikpso_status ikpso_calculate_pso(float* particles, const float* positions, float
         IKPSO_HIP(hipMemcpyAsync(rsnap, randoms, sizeof(ikpso_rng_state) * (size_t)size, hipMemcpyDeviceToDevice, s));
         IKPSO_HIP(carve_coop(io, wsb, cg, cng, cblk, D, s));
         IKPSO_HIP(launch_coop(ch, mode, io, s));
-        int32_t err = 0;
-        IKPSO_HIP(hipMemcpyAsync(&err, io.coop_error, sizeof(err), hipMemcpyDeviceToHost, s));
+        // the error flag (into pinned memory: a truly asynchronous copy) and the
+        // answer come back behind ONE synchronisation; a fallback rewrites the answer
+        if (!g_err_pinned) IKPSO_HIP(hipHostMalloc(reinterpret_cast<void**>(&g_err_pinned), sizeof(int32_t)));
+        *g_err_pinned = 0;
+        IKPSO_HIP(hipMemcpyAsync(g_err_pinned, io.coop_error, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+        IKPSO_HIP(hipMemcpyAsync(result, dres, sizeof(float) * D, hipMemcpyDefault, s));
         IKPSO_HIP(hipStreamSynchronize(s));
-        if (err) {
+        if (!*g_err_pinned) return IKPSO_OK;
+        {
             // The group could not assemble (other work held CUs): restore the
             // generator states and solve on the streaming kernels, which need
             // no co-residency -- the caller never sees the contention.
