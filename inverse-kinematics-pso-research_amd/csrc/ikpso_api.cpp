@@ -8,6 +8,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
+
 #include <array>
 #include <atomic>
 #include <mutex>
@@ -516,14 +518,27 @@ int env_kernel()
 // still gets its own CUs), G chunks per swarm, NG concurrent groups (a
 // multiple of 8 for the XCD-aware membership, kCoopBlocksPerCU workgroups per CU, at most
 // ceil8(B)).  False if infeasible.
-bool coop_plan(const ChainHost& ch, int mode, int P, int64_t B, bool latency, int* G, int* NG, int* block)
+// *linear: a latency group wider than an XCD (G > CUs / 8: the visualiser's N =
+// 16384 is 64 chunks) spans XCDs with linear membership (group = workgroup / G,
+// NG = CUs / G, not a multiple of 8); its hand-offs cross XCDs (agent-scope
+// granules are coherent there, MI355X_MICROARCH: +0.1-0.3 us per hop).
+bool coop_plan(const ChainHost& ch, int mode, int P, int64_t B, bool latency, int* G, int* NG, int* block,
+               bool* linear = nullptr)
 {
     CoopGeometry geo;
     if (!coop_geometry(ch, mode, &geo)) return false;
     int T = geo.threads;
+    if (linear) *linear = false;
     if (latency && geo.latency_variant) {
         const int gl = (P + kCoopLatencyThreads - 1) / kCoopLatencyThreads;
         if (gl <= 64 && B * gl <= (int64_t)geo.cus && ((geo.cus / gl) & ~7) >= 8) T = kCoopLatencyThreads;
+        if (linear && T != kCoopLatencyThreads && gl <= 64 && B * gl <= (int64_t)geo.cus && coop_latency_split(ch)) {
+            *G = gl;
+            *NG = (int)std::min<int64_t>(B, geo.cus / gl);
+            *block = kCoopLatencyThreads;
+            *linear = true;
+            return true;
+        }
     }
     const int g = (P + T - 1) / T;
     int ng = (geo.cus * geo.blocks_per_cu / g) & ~7;
@@ -561,9 +576,10 @@ uint32_t coop_spin_limit()
 
 // Point the coop fields of `io` into workspace `ws` (coop_workspace_bytes) and
 // clear the counters and the error flag.
-hipError_t carve_coop(SwarmIO& io, void* ws, int G, int NG, int block, int D, hipStream_t s)
+hipError_t carve_coop(SwarmIO& io, void* ws, int G, int NG, int block, int D, hipStream_t s, bool linear = false)
 {
     io.coop_spin_limit = coop_spin_limit();
+    io.coop_linear = linear ? 1 : 0;
     Carver cv{static_cast<char*>(ws)};
     io.coop_error = cv.take<int32_t>(1);
     io.coop_slots = cv.take<unsigned long long>((size_t)NG * 2 * G * kCoopSlot(D));
@@ -631,6 +647,7 @@ struct ikpso_solver {
         const int32_t* error = nullptr;  // device flag in ws
     } pending;
     int64_t fallbacks = 0;
+    int32_t* err_host = nullptr;  // pinned host copy of a cooperative solve's error flag (ikpso_solver_sync)
 #if IKPSO_COOP_TIMING
     unsigned long long* pending_timing = nullptr;
     int pending_timing_n = 0;
@@ -755,8 +772,9 @@ ikpso_status ikpso_calculate_pso(float* particles, const float* positions, float
     if (family == IKPSO_KERNEL_RESIDENT && env_kernel() == IKPSO_KERNEL_AUTO && prefer_latency_coop(ch, mode, size, 1))
         family_run = IKPSO_KERNEL_COOP;
     int cg = 0, cng = 0, cblk = 0;
+    bool clin = false;
     if (family_run == IKPSO_KERNEL_COOP &&
-        !coop_plan(ch, mode, size, 1, env_kernel() == IKPSO_KERNEL_AUTO, &cg, &cng, &cblk))
+        !coop_plan(ch, mode, size, 1, env_kernel() == IKPSO_KERNEL_AUTO, &cg, &cng, &cblk, &clin))
         return IKPSO_ERR_UNSUPPORTED;
 
     std::lock_guard<std::mutex> lk(g_scratch_mu);
@@ -801,7 +819,7 @@ ikpso_status ikpso_calculate_pso(float* particles, const float* positions, float
         ikpso_rng_state* rsnap =
             reinterpret_cast<ikpso_rng_state*>(wsb + ((coop_workspace_bytes(cng, cg, D, cblk) + 255) & ~size_t(255)));
         IKPSO_HIP(hipMemcpyAsync(rsnap, randoms, sizeof(ikpso_rng_state) * (size_t)size, hipMemcpyDeviceToDevice, s));
-        IKPSO_HIP(carve_coop(io, wsb, cg, cng, cblk, D, s));
+        IKPSO_HIP(carve_coop(io, wsb, cg, cng, cblk, D, s, clin));
         IKPSO_HIP(launch_coop(ch, mode, io, s));
         // the error flag (into pinned memory: a truly asynchronous copy) and the
         // answer come back behind ONE synchronisation; a fallback rewrites the answer
@@ -944,6 +962,7 @@ ikpso_status ikpso_solver_destroy(ikpso_solver* s)
     const ikpso_status pend = s->pending.active ? ikpso_solver_sync(s) : IKPSO_OK;
     if (s->rng) (void)hipFree(s->rng);
     if (s->rng_snap) (void)hipFree(s->rng_snap);
+    if (s->err_host) (void)hipHostFree(s->err_host);
     if (s->aux) (void)hipFree(s->aux);
     if (s->aux_dh) (void)hipFree(s->aux_dh);
     if (s->ws) (void)hipFree(s->ws);
@@ -1006,7 +1025,8 @@ ikpso_status ikpso_solve_batch(ikpso_solver* s, const float* targets, const floa
     const int D = ch.kernel_dims();
     if (s->family == IKPSO_KERNEL_COOP || latency_coop) {
         int G, NG, T;
-        if (!coop_plan(ch, s->mode, s->P, num_swarms, s->requested == IKPSO_KERNEL_AUTO, &G, &NG, &T))
+        bool linear = false;
+        if (!coop_plan(ch, s->mode, s->P, num_swarms, s->requested == IKPSO_KERNEL_AUTO, &G, &NG, &T, &linear))
             return IKPSO_ERR_UNSUPPORTED;
         ikpso_status st = grow(&s->ws, &s->ws_bytes, coop_workspace_bytes(NG, G, D, T));
         if (st != IKPSO_OK) return st;
@@ -1031,7 +1051,8 @@ ikpso_status ikpso_solve_batch(ikpso_solver* s, const float* targets, const floa
         io.P = s->P;
         io.iterations = iterations;
         io.num_swarms = num_swarms;
-        IKPSO_HIP(carve_coop(io, s->ws, G, NG, T, D, hs));
+        IKPSO_HIP(carve_coop(io, s->ws, G, NG, T, D, hs, linear));
+        s->last_latency = T == kCoopLatencyThreads;  // the reported name follows the variant that runs
         IKPSO_HIP(launch_coop(ch, s->mode, io, hs));
         s->pending.active = true;
         s->pending.targets = targets;
@@ -1059,9 +1080,12 @@ ikpso_status ikpso_solver_sync(ikpso_solver* s)
     if (!s->pending.active) return IKPSO_OK;
     auto& p = s->pending;
     p.active = false;
-    int32_t err = 0;
-    IKPSO_HIP(hipMemcpyAsync(&err, p.error, sizeof(err), hipMemcpyDeviceToHost, p.stream));
+    // into pinned memory: a truly asynchronous copy, one synchronisation
+    if (!s->err_host) IKPSO_HIP(hipHostMalloc(reinterpret_cast<void**>(&s->err_host), sizeof(int32_t)));
+    *s->err_host = 0;
+    IKPSO_HIP(hipMemcpyAsync(s->err_host, p.error, sizeof(int32_t), hipMemcpyDeviceToHost, p.stream));
     IKPSO_HIP(hipStreamSynchronize(p.stream));
+    const int32_t err = *s->err_host;
 #if IKPSO_COOP_TIMING
     if (s->pending_timing) {  // measurement build: mean cycles per iteration over the workgroups
         std::vector<unsigned long long> t((size_t)s->pending_timing_n * 8);

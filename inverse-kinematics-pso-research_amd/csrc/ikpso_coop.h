@@ -30,7 +30,9 @@
 // exchange, by which time every chunk has finished reading parity p.  The
 // slots are zeroed before every launch (tag 0 never matches).  Workgroup b sits
 // on XCD b % 8; the G chunks of a group share an XCD (speed only, never
-// correctness).  Waits are bounded: a timed-out wait sets io.coop_error and
+// correctness) -- except a latency group wider than an XCD (the visualiser's
+// N = 16384: 64 chunks), which takes linear membership and hands off across
+// XCDs (coop_membership).  Waits are bounded: a timed-out wait sets io.coop_error and
 // the kernel drains.
 // Residency is checked at launch against the occupancy query.
 #pragma once
@@ -75,6 +77,22 @@ struct CoopShared {
     unsigned int n_imp, n_remote, n_polls;  // improving exchanges, ... won by another chunk, key polls
 #endif
 };
+
+// Group membership of a cooperative workgroup: XCD-aware (workgroups b, b+8,
+// b+16, ... share an XCD, so a group's chunks share an L2) or, for a latency
+// group wider than an XCD, linear.
+__device__ __forceinline__ void coop_membership(const SwarmIO& io, int* group, int* member)
+{
+    const int G = io.coop_g;
+    if (io.coop_linear) {
+        *group = blockIdx.x / G;
+        *member = blockIdx.x % G;
+    } else {
+        const int xcd = blockIdx.x & 7, pos = blockIdx.x >> 3;
+        *group = (pos / G) * 8 + xcd;
+        *member = pos % G;
+    }
+}
 
 // Exchange `e` of a group: publish this chunk's local argmin, wait for the G
 // chunks, reduce; returns the group-wide minimum key of this exchange (uniform)
@@ -214,12 +232,11 @@ __global__ void __launch_bounds__(BLOCK, (kCoopMinWaves<Topo::D, BLOCK, TERMS>))
     CoopShared<J>& cs = lds.extra;
     float* const s_pb = lds.pb;
     if (tid == 0) {
-        // XCD-aware group membership: workgroups b, b+8, b+16, ... share an XCD
         const int G = io.coop_g;
-        const int xcd = blockIdx.x & 7, pos = blockIdx.x >> 3;
-        const int group = (pos / G) * 8 + xcd;
+        int group, member;
+        coop_membership(io, &group, &member);
         cs.G = G;
-        cs.member = pos % G;
+        cs.member = member;
         cs.e = 0;
         cs.abort = 0;
         cs.b = group;
@@ -369,8 +386,8 @@ inline hipError_t launch_coop_block(const ChainConsts<Topo::J>& cc, const SwarmI
     const int fit = per_cu < want_per_cu ? per_cu : want_per_cu;
     if (fit < 1) return hipErrorCooperativeLaunchTooLarge;
     SwarmIO run = io;
-    const int ng_fit = (int)(((int64_t)cus * fit / io.coop_g) & ~int64_t(7));
-    if (ng_fit < 8) return hipErrorCooperativeLaunchTooLarge;
+    const int ng_fit = io.coop_linear ? cus * fit / io.coop_g : (int)(((int64_t)cus * fit / io.coop_g) & ~int64_t(7));
+    if (ng_fit < (io.coop_linear ? 1 : 8)) return hipErrorCooperativeLaunchTooLarge;
     if (run.coop_ng > ng_fit) run.coop_ng = ng_fit;
     const int64_t grid = (int64_t)run.coop_ng * run.coop_g;
     hipLaunchKernelGGL(kernel, dim3((unsigned)grid), dim3(T), 0, stream, cc, run);
@@ -503,10 +520,10 @@ __global__ void __launch_bounds__(2 * kCoopLatencyThreads) k_swarm_coop_split(co
     const int P = io.P;
     if (tid == 0) {
         const int G = io.coop_g;
-        const int xcd = blockIdx.x & 7, pos = blockIdx.x >> 3;
-        const int group = (pos / G) * 8 + xcd;
+        int group, member;
+        coop_membership(io, &group, &member);
         cs.G = G;
-        cs.member = pos % G;
+        cs.member = member;
         cs.e = 0;
         cs.abort = 0;
         cs.b = group;
@@ -654,8 +671,8 @@ inline hipError_t launch_coop_split(const ChainConsts<Topo::J>& cc, const SwarmI
     if (e != hipSuccess) return e;
     if (per_cu < 1) return hipErrorCooperativeLaunchTooLarge;
     SwarmIO run = io;
-    const int ng_fit = (int)(((int64_t)cus / io.coop_g) & ~int64_t(7));
-    if (ng_fit < 8) return hipErrorCooperativeLaunchTooLarge;
+    const int ng_fit = io.coop_linear ? cus / io.coop_g : (int)(((int64_t)cus / io.coop_g) & ~int64_t(7));
+    if (ng_fit < (io.coop_linear ? 1 : 8)) return hipErrorCooperativeLaunchTooLarge;
     if (run.coop_ng > ng_fit) run.coop_ng = ng_fit;
     const int64_t grid = (int64_t)run.coop_ng * run.coop_g;
     hipLaunchKernelGGL(kernel, dim3((unsigned)grid), dim3(T), 0, stream, cc, run);

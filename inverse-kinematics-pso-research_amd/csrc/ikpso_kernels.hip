@@ -116,8 +116,8 @@ hipError_t launch_evaluate(const ChainHost& ch, int mode, const EvalIO& io, hipS
 hipError_t launch_coop(const ChainHost& ch, int mode, const SwarmIO& io, hipStream_t stream)
 {
     if (io.num_swarms <= 0) return hipSuccess;
-    if (!ch.aux_dev || io.coop_g <= 0 || io.coop_ng <= 0 || io.coop_ng % 8 != 0 || !io.coop_slots ||
-        !io.coop_error)
+    if (!ch.aux_dev || io.coop_g <= 0 || io.coop_ng <= 0 || (!io.coop_linear && io.coop_ng % 8 != 0) ||
+        !io.coop_slots || !io.coop_error)
         return hipErrorInvalidValue;
     hipError_t err = hipErrorInvalidValue;
     const bool ok = visit_topology(ch, [&](auto topo) {

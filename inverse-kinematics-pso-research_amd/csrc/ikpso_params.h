@@ -76,6 +76,8 @@ struct SwarmIO {
     int32_t coop_block;       // workgroup size (kCoopThreads<J>() or kCoopLatencyThreads)
     uint32_t coop_spin_limit; // polls before a group wait gives up (0: give up at the first unmet poll)
     unsigned long long* coop_timing;  // IKPSO_COOP_TIMING builds: [NG*G][4] cycle counts (else null)
+    int32_t coop_linear;      // membership: 0 = XCD-aware (a group on one XCD, NG a multiple of 8),
+                              // 1 = linear (group = workgroup / G: a latency group wider than an XCD)
 };
 
 // Streaming (state-in-HBM) kernels: one launch per PSO iteration over every

@@ -74,11 +74,27 @@ def test_coop_equals_streaming(device):
 
 
 def test_coop_visualiser_swarm_auto(oracle, device, monkeypatch):
-    """AUTO picks the cooperative kernel for the visualiser's N = 16384."""
+    """AUTO picks the cooperative kernel for the visualiser's N = 16384; a few
+    such swarms run the latency variant with generator waves, each swarm's 64
+    chunks a group wider than an XCD (linear membership, cross-XCD hand-offs):
+    REFERENCE bit-exact to the oracle, and a full batch goes back to the
+    throughput plan."""
     chain = ikpso.reference_scene(reset=True).origin.to_cuda()
-    s = ikpso.BatchSolver(chain, 16384)
+    B, P, I = 2, 16384, 5
+    s = ikpso.BatchSolver(chain, P, pso=ikpso.PSOConfig(0.5, 0.5, 1.25, I), arith="reference")
     assert "coop" in s.kernel
+    tg = ikpso.workload(3).targets(0, B)
+    s.seed(8)
+    ang, fit, res = (t.cpu().numpy() for t in s.solve(dev(tg), iterations=I))
+    assert s.kernel == "swarm_coop<ref_tree7> (latency variant, generator waves)", s.kernel
+    states = s.generator_states(0, B)
+    s.solve(dev(ikpso.workload(3).targets(0, 8)), iterations=1)
+    assert s.kernel == "swarm_coop<ref_tree7>", s.kernel
     s.close()
+    ostate = oracle.init_generators(B * P, 0)
+    oang, ofit, ores = oracle.solve_batch(chain, tg, None, P, I, ostate, threads=8)
+    assert np.array_equal(ang, oang) and np.array_equal(fit, ofit)
+    assert np.array_equal(states[:, :6], ostate.view(np.int32).reshape(B * P, 12)[:, :6])
 
 
 def test_auto_reports_latency_variant(device):
