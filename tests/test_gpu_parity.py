@@ -150,7 +150,7 @@ def test_calculate_pso_one_step(oracle, device, scene_chain, monkeypatch, arith)
 
 @pytest.mark.parametrize("kernel", KERNELS)
 @pytest.mark.parametrize("arith", ["fast", "reference"])
-@pytest.mark.parametrize("P,I", [(256, 20), (1024, 20), (700, 13)])
+@pytest.mark.parametrize("P,I", [(256, 20), (1024, 20), (700, 13), (65, 20)])
 def test_tier_a(oracle, device, scene_chain, monkeypatch, arith, P, I, kernel):
     monkeypatch.setenv("IKPSO_ARITH", arith)
     monkeypatch.setenv("IKPSO_KERNEL", kernel)
