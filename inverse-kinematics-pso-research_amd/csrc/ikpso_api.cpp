@@ -1052,7 +1052,10 @@ ikpso_status ikpso_solve_batch(ikpso_solver* s, const float* targets, const floa
         io.iterations = iterations;
         io.num_swarms = num_swarms;
         IKPSO_HIP(carve_coop(io, s->ws, G, NG, T, D, hs, linear));
-        s->last_latency = T == kCoopLatencyThreads;  // the reported name follows the variant that runs
+        // the reported name follows the variant that runs (long chains' throughput chunks are
+        // kCoopLatencyThreads wide too: only a block other than the throughput one is the latency plan)
+        CoopGeometry geo;
+        s->last_latency = coop_geometry(ch, s->mode, &geo) && T != geo.threads;
         IKPSO_HIP(launch_coop(ch, s->mode, io, hs));
         s->pending.active = true;
         s->pending.targets = targets;

@@ -39,6 +39,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <mutex>
 #include <type_traits>
 
 #include "ikpso_resident.h"
@@ -366,6 +367,33 @@ __global__ void __launch_bounds__(BLOCK, (kCoopMinWaves<Topo::D, BLOCK, TERMS>))
     }
 }
 
+// The device's CU count and a kernel's resident workgroups per CU, queried once per
+// (kernel, device) -- a latency-bound caller (the visualiser's per-frame call)
+// launches thousands of times.
+struct ResidencyCache {
+    std::mutex mu;
+    int dev = -1, cus = 0, per_cu = 0;
+};
+// `cache` is the launching function's own static: one per kernel instantiation.
+template <class K>
+inline hipError_t coop_residency(ResidencyCache& cache, K kernel, int threads, int* cus, int* per_cu)
+{
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    std::lock_guard<std::mutex> lk(cache.mu);
+    if (dev != cache.dev) {
+        int n = 0, p = 0;
+        e = hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+        if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&p, kernel, threads, 0);
+        if (e != hipSuccess) return e;
+        cache.dev = dev, cache.cus = n, cache.per_cu = p;
+    }
+    *cus = cache.cus;
+    *per_cu = cache.per_cu;
+    return hipSuccess;
+}
+
 // Launch: grid = NG * G workgroups, at most kCoopBlocksPerCU per CU.  Co-residency is
 // checked here against the occupancy query (the check hipLaunchCooperativeKernel
 // would make; a plain launch gives the same residency without the cooperative
@@ -374,10 +402,9 @@ template <class Topo, int MODE, int TERMS, int T>
 inline hipError_t launch_coop_block(const ChainConsts<Topo::J>& cc, const SwarmIO& io, hipStream_t stream)
 {
     const auto kernel = &k_swarm_coop<Topo, MODE, TERMS, T>;
-    int dev = 0, cus = 0, per_cu = 0;
-    hipError_t e = hipGetDevice(&dev);
-    if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, T, 0);
+    static ResidencyCache cache;
+    int cus = 0, per_cu = 0;
+    const hipError_t e = coop_residency(cache, kernel, T, &cus, &per_cu);
     if (e != hipSuccess) return e;
     // The plan assumed kCoopBlocksPerCU workgroups per CU; a build whose registers
     // admit fewer (the long chains' collider builds exceed 256 VGPRs) runs fewer
@@ -664,10 +691,9 @@ inline hipError_t launch_coop_split(const ChainConsts<Topo::J>& cc, const SwarmI
 {
     const auto kernel = &k_swarm_coop_split<Topo, MODE, TERMS>;
     constexpr int T = 2 * kCoopLatencyThreads;
-    int dev = 0, cus = 0, per_cu = 0;
-    hipError_t e = hipGetDevice(&dev);
-    if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, T, 0);
+    static ResidencyCache cache;
+    int cus = 0, per_cu = 0;
+    const hipError_t e = coop_residency(cache, kernel, T, &cus, &per_cu);
     if (e != hipSuccess) return e;
     if (per_cu < 1) return hipErrorCooperativeLaunchTooLarge;
     SwarmIO run = io;

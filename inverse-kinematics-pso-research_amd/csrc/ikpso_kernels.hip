@@ -13,6 +13,7 @@
 //     (randInitKernel, src/utility_kernels.cuh:21-31).
 #include <hip/hip_runtime.h>
 
+#include <mutex>
 #include <string>
 #include <type_traits>
 
@@ -145,10 +146,19 @@ bool coop_geometry(const ChainHost& ch, int mode, CoopGeometry* g)
         }
     });
     if (!spec) return false;
-    int dev = 0, cus = 0;
+    // the CU count, once per device (the plan runs on every latency-bound call)
+    static std::mutex mu;
+    static int c_dev = -1, c_cus = 0;
+    int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return false;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) return false;
-    g->cus = cus;
+    std::lock_guard<std::mutex> lk(mu);
+    if (dev != c_dev) {
+        int cus = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+            return false;
+        c_dev = dev, c_cus = cus;
+    }
+    g->cus = c_cus;
     return true;
 }
 

@@ -68,6 +68,7 @@ def test_config5_reference_bitexact_g8(oracle, device):
     s.seed(B)
     tg, oang, ofit, ores, ostate = oracle_batch(oracle, wl, B, I)
     ang, fit, res = (t.cpu().numpy() for t in s.solve(dev(tg), iterations=I))
+    assert s.kernel == "swarm_coop<serial_tip20>", s.kernel  # the throughput plan (not the latency name)
     states = s.generator_states(0, B)
     s.close()
     assert np.array_equal(states[:, :6], words(ostate))  # D + 3*D*I draws per particle
@@ -84,6 +85,7 @@ def test_config5_fast_tier_b_own_size(oracle, device):
     s.seed(B)
     tg, oang, ofit, ores, ostate = oracle_batch(oracle, wl, B, I)
     ang, fit, res = (t.cpu().numpy() for t in s.solve(dev(tg), iterations=I))
+    assert s.kernel == "swarm_coop<serial_tip20>", s.kernel  # the throughput plan (not the latency name)
     states = s.generator_states(0, B)
     s.close()
     assert np.array_equal(states[:, :6], words(ostate))
