@@ -28,9 +28,11 @@ constexpr int kTrigAheadMaxD = 30;
 // Progress-levelled wave priority (progress_prio): levels of the 2-wave steps
 // and of the pipelined 4-wave step.  Measured: config 5 81.1 -> 77.4 ms on 2048
 // swarms x 100 iterations with 4 levels (profiles/r02c, r02d variant_timings);
-// config 3 48.3 -> 47.3 ms with 2 levels, 51.7 ms with 4 (profiles/r02g); the
-// folded DH arm's 4-wave tip-backward step unchanged within noise (so none).
-constexpr int kPrioLevels2Wave = 4, kPrioLevels4Wave = 2;
+// with two chunks of different swarms per CU (round 3) 3 levels are better:
+// 4 / 3 / 2 / none 61.2 / 60.2 / 61.9 / 67.2 ms (profiles/r03s); config 3 48.3
+// -> 47.3 ms with 2 levels, 51.7 ms with 4 (profiles/r02g); the folded DH arm's
+// 4-wave tip-backward step unchanged within noise (so none).
+constexpr int kPrioLevels2Wave = 3, kPrioLevels4Wave = 2;
 
 // Progress-levelled wave priority: entering node k of J a wave sets its issue
 // priority to (L-1) - L(k-1)/J, so a wave that has run ahead of the others on
