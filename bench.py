@@ -10,6 +10,11 @@ timed region.  Weak scaling: per-GPU work is fixed, N GPUs solve N x 4096
 targets (N = 8 is 32768 targets; `--swarms-per-gpu 8192` gives config 4's
 65536).  Generator seeds are global (swarm b, particle i: curand_init(b*1024+i)).
 
+With the default config 3 the same run also times, every rank, the other
+BASELINE lines under "legs": config 4's shard (8192 targets per GPU, so N = 8
+is the named 65536), config 5 at its named size (8192 targets of the 20-joint
+chain over all GPUs) and the DH arm (dh7); `--extra-steps 0` skips them.
+
 Prints ONE JSON line on rank 0 (see DESIGN.md for every field).
 """
 from __future__ import annotations
@@ -56,6 +61,11 @@ def parse():
     ap.add_argument("--reference-steps", type=int, default=3,
                     help="after the FAST legs, time this many steps of the same workload in REFERENCE arithmetic "
                          "(the bit-exact path; rank 0, configs 3/4; 0 = skip)")
+    ap.add_argument("--extra-legs", default="4,5,dh7",
+                    help="with the default config 3: also time these BASELINE lines in the same run and print them "
+                         "under 'legs' (4 = config 4's 8192 targets per GPU, 5 = config 5, dh7 = the DH arm)")
+    ap.add_argument("--extra-steps", type=int, default=2, help="timed steps per extra leg (0 = no extra legs)")
+    ap.add_argument("--extra-warmup", type=int, default=1)
     ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
                     help="gloo: rehearse the N>1 path with ranks sharing the visible GPUs (not a measurement)")
     return ap.parse_args()
@@ -193,6 +203,129 @@ def cpu_baseline(seconds: float, threads: int, dh=None):
                                   f"{e5:.1f} s"}}
 
 
+def timed_leg(ctx, wl, Bl, P, I, steps, warmup, arith="fast", kernel="auto"):
+    """One workload timed the driver's way on every rank: W untimed steps, then
+    K steps between barrier + synchronize on both sides, max over ranks.  A step
+    = one batch of Bl swarms per rank (ONE solver launch) + the all-gather of
+    the per-swarm results + the copy to the host.  Returns the solver too (the
+    caller closes it)."""
+    torch, dist, ikpso, idist, dev, world, rank = (ctx[k] for k in
+                                                   ("torch", "dist", "ikpso", "idist", "dev", "world", "rank"))
+    import numpy as np
+
+    total, first = Bl * world, rank * Bl
+    targets = torch.from_numpy(wl.targets(first, Bl)).to(dev)
+    solver = ikpso.BatchSolver(wl.chain, P, pso=ikpso.PSOConfig(0.5, 0.5, 1.25, I), fit=wl.fit, arith=arith,
+                               limit_weight=wl.limit_weight, soft_lo=wl.soft_lo, soft_hi=wl.soft_hi,
+                               kernel=kernel, axis_mask=wl.axis_mask, fold=wl.fold)
+    solver.seed(Bl, seed_base=0, first_swarm=first)
+    D = solver.dof
+    out = (torch.empty((Bl, D), device=dev), torch.empty((Bl,), device=dev), torch.empty((Bl,), device=dev))
+    host = torch.empty((total, D + 2), dtype=torch.float32, pin_memory=True)
+
+    def step(evs=None):
+        if evs is not None:
+            evs[0].record()
+        solver.solve(targets, iterations=I, out=out)
+        if evs is not None:
+            evs[1].record()
+        rows = idist.pack_results(*out)
+        if world > 1:
+            rows = idist.gather_rows(rows, total, world)
+        host.copy_(rows, non_blocking=True)
+
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    t0 = time.perf_counter()
+    for k in range(steps):
+        step(evs[k])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device="cpu" if ctx["backend"] == "gloo" else dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    res = host.numpy()
+    return {"elapsed": float(t[0]), "kern_ms": float(t[1]), "solver": solver, "D": D, "total": total,
+            "targets": targets, "first": first, "finite": bool(np.isfinite(res).all()),
+            "mean_fitness": float(res[:, D].mean()), "mean_residual": float(res[:, D + 1].mean())}
+
+
+def valu_roofline(kernel: str, ups_launch: float, kern_ms: float, lib_id: str):
+    """VALU lane-instructions per update (rocprofv3 SQ_INSTS_VALU x 64 / updates, committed in
+    profiles/valu_per_update.json) x the live update rate, against the chip's 78.6 T lane-instructions/s
+    (256 CU x 4 SIMD x 32 lanes x 2.4 GHz: every wave64 VALU op at its 2-cycle full rate).  None for a kernel
+    without committed counters (or a streaming one: HBM-bound, priced by the caller)."""
+    vpu = None if "streaming" in kernel else valu_per_update(kernel)
+    if not vpu:
+        return None, None
+    kern_s = kern_ms / 1e3
+    instr = vpu["valu_lane_instr_per_update"]
+    ach = ups_launch * instr / kern_s / 1e12
+    # Secondary views.  gfx950 issue costs are not uniform (tools/probes/valu_probe.hip,
+    # profiles/r02/valu_issue_costs.txt): v_lshlrev, v_add3, v_cvt, v_med3/max3 ... occupy 4.1 cycles,
+    # v_sin/v_cos 8.1; the issue model (tools/issue_model.py on the kernel's ISA) prices the hot loop
+    # opcode by opcode -- a roof lowered to the kernel's own instruction mix, not the chip's.
+    trans = vpu.get("trans_lane_instr_per_update") or 0.0
+    model = vpu.get("issue_model")
+    slots_simple = instr + 3.0 * trans
+    slots = instr * model["mean_cycles_per_instr"] / 2.0 if model else None
+    valu = {"achieved": round(ach, 2), "peak": round(VALU_PEAK_TINSTR, 1), "unit": "Tlane-instr/s",
+            "frac": round(ach / VALU_PEAK_TINSTR, 4),
+            "instr_per_update": instr, "trans_per_update": trans, "source": vpu.get("source"),
+            "measured_on_build": vpu.get("build_id"), "stale": vpu.get("build_id") != lib_id,
+            "frac_issue_model": round(ups_launch * slots / kern_s / 1e12 / VALU_PEAK_TINSTR, 4)
+            if slots else None,
+            "issue_slots_per_update": round(slots, 1) if slots else None, "issue_model": model,
+            "frac_uniform_cost": round(ups_launch * slots_simple / kern_s / 1e12 / VALU_PEAK_TINSTR, 4),
+            "note": "frac = SQ_INSTS_VALU lane-instructions per update x updates/s / 78.6 T (chip peak, "
+                    "every op at full rate); frac_issue_model: the same time priced at each opcode's "
+                    "measured gfx950 issue cost (4-cycle integer/convert/med3 forms, 8-cycle sin/cos) -- "
+                    "the fraction of the SIMDs' issue cycles the kernel's own mix keeps busy; "
+                    "frac_uniform_cost: transcendentals as 4 slots. stale: the counters were measured on "
+                    "another build than the loaded library"}
+    return vpu, valu
+
+
+def extra_leg(ctx, name, steps, warmup, lib_id, cpu=None):
+    """Another BASELINE line measured in the same run (every rank, same timing rules as the headline):
+    4 = config 4's shard, 8192 targets per GPU (N = 8: the named 65536); 5 = config 5, its named 8192 targets
+    over all GPUs; dh7 = the DH arm, 4096 targets per GPU."""
+    ikpso, world = ctx["ikpso"], ctx["world"]
+    wl = ikpso.workload(name)
+    if name == "4":
+        Bl, wname = 8192, "config 4 (8192 targets per GPU; 65536 at N = 8)"
+    elif name == "5":
+        Bl, wname = -(-wl.swarms // world), "config 5 (8192 targets over all GPUs)"
+    else:
+        Bl, wname = wl.swarms, f"{name} (4096 targets per GPU)"
+    P, I = wl.particles, wl.iterations
+    r = timed_leg(ctx, wl, Bl, P, I, steps, warmup)
+    ups_launch = Bl * P * I
+    _, valu = valu_roofline(r["solver"].kernel, ups_launch, r["kern_ms"], lib_id)
+    leg = {"workload": f"{wname}: {wl.description}; {P} particles, {I} iterations",
+           "value": r["total"] * P * I * steps / r["elapsed"], "unit": "particle-updates/s",
+           "solves_per_s": r["total"] * steps / r["elapsed"], "ms_per_step": 1e3 * r["elapsed"] / steps,
+           "kernel_ms": round(r["kern_ms"], 3), "steps": steps, "warmup": warmup, "swarms_per_gpu": Bl,
+           "total_swarms": r["total"], "dof": r["D"], "kernel": r["solver"].kernel,
+           "roofline_frac": valu["frac"] if valu else None,
+           "roofline_frac_issue_model": valu["frac_issue_model"] if valu else None,
+           "roofline_stale": valu["stale"] if valu else None,
+           "check": {"finite": r["finite"], "mean_fitness": r["mean_fitness"], "mean_residual": r["mean_residual"]}}
+    if cpu is not None:
+        leg["cpu_baseline"] = cpu
+    r["solver"].close()
+    return leg
+
+
 def main():
     args = parse()
     launch_ranks(args)
@@ -215,6 +348,8 @@ def main():
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
+    ctx = {"torch": torch, "dist": dist, "ikpso": ikpso, "idist": idist, "dev": dev, "world": world,
+           "rank": rank, "backend": args.dist_backend}
 
     wl = ikpso.workload(args.config)
     cfg = int(args.config) if args.config.isdigit() else args.config
@@ -226,30 +361,8 @@ def main():
         Bl = wl.swarms                      # weak scaling: 4096 per GPU
     else:
         Bl = -(-wl.swarms // world)         # configs 4/5: the named total over all GPUs
-    total = Bl * world
-    first = rank * Bl
-    targets = torch.from_numpy(wl.targets(first, Bl)).to(dev)
-    solver = ikpso.BatchSolver(wl.chain, P, pso=ikpso.PSOConfig(0.5, 0.5, 1.25, I), fit=wl.fit, arith=args.arith,
-                               limit_weight=wl.limit_weight, soft_lo=wl.soft_lo, soft_hi=wl.soft_hi,
-                               kernel=args.kernel, axis_mask=wl.axis_mask, fold=wl.fold)
-    solver.seed(Bl, seed_base=0, first_swarm=first)
-    D = solver.dof
-    out = (torch.empty((Bl, D), device=dev), torch.empty((Bl,), device=dev), torch.empty((Bl,), device=dev))
-    host = torch.empty((total, D + 2), dtype=torch.float32, pin_memory=True)
 
-    def step(evs=None):
-        if evs is not None:
-            evs[0].record()
-        solver.solve(targets, iterations=I, out=out)
-        if evs is not None:
-            evs[1].record()
-        rows = idist.pack_results(*out)
-        if world > 1:
-            rows = idist.gather_rows(rows, total, world)
-        host.copy_(rows, non_blocking=True)
-
-    # the bounded CPU baseline runs before the GPU legs (rank 0, N = 1), so the timed GPU loop is the
-    # process's last long phase (an external utilisation sampler sees the GPU busy at the end)
+    # the bounded CPU baseline runs before the GPU legs (rank 0, N = 1)
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0 and cfg in (3, 5, "dh7", "dh7-nofold", "dh7-locked"):
         cpu = cpu_baseline(args.cpu_seconds, args.cpu_threads, dh=wl if isinstance(cfg, str) else None)
@@ -258,35 +371,12 @@ def main():
         if isinstance(cfg, str):  # the DH arm's own figure
             cpu = dict(cpu, value=cpu["dh"]["value"], sample=cpu["dh"]["sample"])
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    t0 = time.perf_counter()
-    for k in range(args.steps):
-        step(evs[k])
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
-    t = torch.tensor([elapsed, kern_ms], dtype=torch.float64,
-                     device="cpu" if args.dist_backend == "gloo" else dev)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed, kern_ms = float(t[0]), float(t[1])
-
+    main_leg = timed_leg(ctx, wl, Bl, P, I, args.steps, args.warmup, args.arith, args.kernel)
+    solver, D, total = main_leg["solver"], main_leg["D"], main_leg["total"]
+    elapsed, kern_ms = main_leg["elapsed"], main_leg["kern_ms"]
+    targets, first = main_leg["targets"], main_leg["first"]
     ups_step = total * P * I
     value = ups_step * args.steps / elapsed
-    # results sanity: finite, and the gathered rows are what each rank solved
-    res = host.numpy()
-    finite = bool(np.isfinite(res).all())
-    mean_fit = float(res[:, D].mean())
-    mean_res = float(res[:, D + 1].mean())
 
     single_ms = None
     if rank == 0 and cfg != 5:
@@ -323,14 +413,31 @@ def main():
             b.record()
         torch.cuda.synchronize()
         el_r = time.perf_counter() - tr
+        rk = sr.kernel
+        _, rvalu = valu_roofline(rk, Bl * P * I, float(np.mean([a.elapsed_time(b) for a, b in evr])),
+                                 ikpso.build_id())
         reference_arith = {"value": Bl * P * I * args.reference_steps / el_r, "unit": "particle-updates/s",
                            "kernel_ms": round(float(np.mean([a.elapsed_time(b) for a, b in evr])), 3),
-                           "steps": args.reference_steps, "warmup": 1, "kernel": sr.kernel,
+                           "steps": args.reference_steps, "warmup": 1, "kernel": rk,
+                           "roofline_frac": rvalu["frac"] if rvalu else None,
                            "swarms": Bl, "check_finite": bool(torch.isfinite(out_r[1]).all()),
                            "note": "REFERENCE arithmetic: the reference's 4x4 operation order, no FMA contraction, "
                                    "correctly rounded sin/cos -- bit-identical to the CPU oracle "
-                                   "(tests/test_gpu_parity.py), same workload, rank 0"}
+                                   "(tests/test_gpu_parity.py) and, through it, to the reference's recorded CUDA "
+                                   "run (tests/test_gpu_trajectory.py); same workload, rank 0"}
         sr.close()
+
+    lib_id = ikpso.build_id()
+    # the other BASELINE lines, same run and timing rules (every rank): config 4's per-GPU shard, config 5 at
+    # its named size, the DH arm -- after the headline legs so the GPU stays busy to the end of the run
+    legs = {}
+    if cfg == 3 and args.extra_steps > 0:
+        for name in args.extra_legs.split(","):
+            name = name.strip()
+            if name:
+                c5 = cpu.get("config5") if (cpu and name == "5") else None
+                legs["config" + name if name.isdigit() else name] = extra_leg(
+                    ctx, name, args.extra_steps, args.extra_warmup, lib_id, c5)
 
     if rank == 0:
         ups_launch = Bl * P * I
@@ -338,37 +445,7 @@ def main():
         alg_bytes = 20 * D + 8
         alg_gbs = ups_launch * alg_bytes / kern_s / 1e9
         streaming = "streaming" in solver.kernel
-        vpu = None if streaming else valu_per_update(solver.kernel)
-        valu = None
-        lib_id = ikpso.build_id()
-        if vpu:
-            # VALU lane-instructions per update (rocprofv3 SQ_INSTS_VALU x 64 / updates, committed in
-            # profiles/valu_per_update.json) x the live update rate, against the chip's 78.6 T lane-instructions/s
-            # (256 CU x 4 SIMD x 32 lanes x 2.4 GHz: every wave64 VALU op at its 2-cycle full rate).
-            instr = vpu["valu_lane_instr_per_update"]
-            ach = ups_launch * instr / kern_s / 1e12
-            # Secondary views.  gfx950 issue costs are not uniform (tools/probes/valu_probe.hip,
-            # profiles/r02/valu_issue_costs.txt): v_lshlrev, v_add3, v_cvt, v_med3/max3 ... occupy 4.1 cycles,
-            # v_sin/v_cos 8.1; the issue model (tools/issue_model.py on the kernel's ISA) prices the hot loop
-            # opcode by opcode -- a roof lowered to the kernel's own instruction mix, not the chip's.
-            trans = vpu.get("trans_lane_instr_per_update") or 0.0
-            model = vpu.get("issue_model")
-            slots_simple = instr + 3.0 * trans
-            slots = instr * model["mean_cycles_per_instr"] / 2.0 if model else None
-            valu = {"achieved": round(ach, 2), "peak": round(VALU_PEAK_TINSTR, 1), "unit": "Tlane-instr/s",
-                    "frac": round(ach / VALU_PEAK_TINSTR, 4),
-                    "instr_per_update": instr, "trans_per_update": trans, "source": vpu.get("source"),
-                    "measured_on_build": vpu.get("build_id"), "stale": vpu.get("build_id") != lib_id,
-                    "frac_issue_model": round(ups_launch * slots / kern_s / 1e12 / VALU_PEAK_TINSTR, 4)
-                    if slots else None,
-                    "issue_slots_per_update": round(slots, 1) if slots else None, "issue_model": model,
-                    "frac_uniform_cost": round(ups_launch * slots_simple / kern_s / 1e12 / VALU_PEAK_TINSTR, 4),
-                    "note": "frac = SQ_INSTS_VALU lane-instructions per update x updates/s / 78.6 T (chip peak, "
-                            "every op at full rate); frac_issue_model: the same time priced at each opcode's "
-                            "measured gfx950 issue cost (4-cycle integer/convert/med3 forms, 8-cycle sin/cos) -- "
-                            "the fraction of the SIMDs' issue cycles the kernel's own mix keeps busy; "
-                            "frac_uniform_cost: transcendentals as 4 slots. stale: the counters were measured on "
-                            "another build than the loaded library"}
+        vpu, valu = valu_roofline(solver.kernel, ups_launch, kern_ms, lib_id)
         # the streaming kernels move x/v/pbest through HBM (HBM-bound); an on-chip kernel without a committed
         # PMC profile is reported unmeasured rather than against the HBM formulation it does not use
         on_chip_unmeasured = not streaming and not valu
@@ -432,14 +509,18 @@ def main():
             "single_solve_ms": single_ms,
             "roofline": roofline,
             "reference_arith": reference_arith,
+            "legs": legs or None,
             "cpu_baseline": cpu,
             "build_id": lib_id,
-            "check": {"finite": finite, "mean_fitness": mean_fit, "mean_residual": mean_res},
+            "check": {"finite": main_leg["finite"], "mean_fitness": main_leg["mean_fitness"],
+                      "mean_residual": main_leg["mean_residual"]},
             "parity": f"{args.arith.upper()} arithmetic. REFERENCE mode is bit-identical to the CPU oracle "
-                      "(tests/test_gpu_parity.py); FAST (benchmarked) holds FK |dp| <= 2e-5, tier A |dtheta| <= 1e-4, "
-                      "tier B mean fitness within 0.5 %. The cuRAND XORWOW step is pinned to rocRAND; its "
-                      "curand_init seeding constants are spec-pinned (cuRAND is not in the image), so bit parity "
-                      "with a real CUDA run of the reference is unpinned; FRAMES_3 (KS test) pins the dynamics.",
+                      "(tests/test_gpu_parity.py), and the oracle and the REFERENCE kernels replay the reference's "
+                      "own recorded CUDA run (results.xlsx DEGREES_3: every case start and 506 of 661 frames within "
+                      "1e-5 rad, tests/test_trajectory.py, tests/test_gpu_trajectory.py) -- which pins cuRAND's "
+                      "seeding and uniform mapping, the draw order, update, clamp, FK, fitness and argmin against "
+                      "the reference itself. FAST (benchmarked) holds FK |dp| <= 2e-5, tier A |dtheta| <= 1e-4 "
+                      "(also against the recording), tier B per-swarm bounds (tests/test_gpu_parity.py).",
         }
         if valu:
             line["roofline"]["valu"] = valu

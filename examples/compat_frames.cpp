@@ -13,12 +13,19 @@
 //
 // Host forward kinematics (glm in the reference, src/Node.h:92-102) is a small
 // float 4x4 product here.  usage: compat_frames [cases] [N]
+//
+// compat_frames replay <skip> <frames> [N]: the recorded session of the
+// reference's results.xlsx DEGREES_3 -- `skip` unrecorded frames, then the R key
+// (resetArm) and `frames` solves with the answer fed back, each printed as
+// "frame k: a0 .. a20" (%.9g round-trips float).  tests/test_gpu_examples.py
+// compares frames 70-74 with the recording and the oracle's replay.
 #include <hip/hip_runtime.h>
 
 #include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <vector>
 
 #include "ikpso_compat.h"
@@ -129,8 +136,11 @@ void fill_positions(const NodeCUDA* n, float* positions)  // FillPositions: node
 
 int main(int argc, char** argv)
 {
-    const int cases = argc > 1 ? atoi(argv[1]) : 5;
-    const int N = argc > 2 ? atoi(argv[2]) : 16384;  // src/Main.cpp:17
+    const bool replay = argc > 1 && strcmp(argv[1], "replay") == 0;
+    const int skip = replay && argc > 2 ? atoi(argv[2]) : 0;
+    const int record = replay && argc > 3 ? atoi(argv[3]) : 0;
+    const int cases = replay ? 0 : (argc > 1 ? atoi(argv[1]) : 5);
+    const int N = argc > (replay ? 4 : 2) ? atoi(argv[replay ? 4 : 2]) : 16384;  // src/Main.cpp:17
     float *particles, *bests, *positions;
     curandState_t* randoms;
     NodeCUDA* chain;
@@ -149,6 +159,33 @@ int main(int argc, char** argv)
 
     NodeCUDA arm[8];
     scene(arm);
+    auto solve = [&](int frame, bool print) -> hipError_t {
+        for (int k = 0; k < kNodes; ++k) chain[k] = arm[k];  // ToCUDA
+        fill_positions(arm, positions);
+        const hipError_t st = calculatePSO(particles, positions, bests, randoms, N, chain, pso, fit, result,
+                                           colliders, 0);
+        if (st != hipSuccess) return st;
+        for (int k = 1; k < kNodes; ++k)  // FromCoords
+            arm[k].rotation = make_float3(result->positions[3 * (k - 1)], result->positions[3 * (k - 1) + 1],
+                                          result->positions[3 * (k - 1) + 2]);
+        if (print) {
+            printf("frame %d:", frame);
+            for (int d = 0; d < DEGREES_OF_FREEDOM; ++d) printf(" %.9g", result->positions[d]);
+            printf("\n");
+        }
+        return hipSuccess;
+    };
+    if (replay) {
+        for (int f = 0; f < skip + record; ++f) {
+            if (f == skip) scene(arm);  // R: resetArm, src/Main.cpp:412-418
+            const hipError_t st = solve(f, f >= skip);
+            if (st != hipSuccess) {
+                fprintf(stderr, "calculatePSO failed: %s\n", hipGetErrorString(st));
+                return 2;
+            }
+        }
+        return 0;
+    }
     std::vector<int> frames;
     double solve_ms = 0.0;
     int solves = 0;

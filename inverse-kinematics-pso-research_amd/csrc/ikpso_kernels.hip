@@ -140,7 +140,10 @@ bool coop_geometry(const ChainHost& ch, int mode, CoopGeometry* g)
         using T = decltype(topo);
         if constexpr (!T::kGeneric) {
             g->threads = kCoopThreads<T::D>();
-            g->blocks_per_cu = kCoopBlocksPerCU<T::D>();
+            // the collider builds (which also carry the wide-angle chains, poly_trig) are
+            // compiled for one workgroup per CU (kCoopMinWaves): plan for that residency,
+            // or the launch could not fit the plan's groups
+            g->blocks_per_cu = (ch.num_coll > 0 || ch.poly_trig) ? 1 : kCoopBlocksPerCU<T::D>();
             g->latency_variant = kCoopThreads<T::D>() != kCoopLatencyThreads;
             spec = true;
         }

@@ -133,6 +133,57 @@ void orc_init_generators(orc_rng* randoms, int64_t size, uint64_t seed_base)
     for (int64_t i = 0; i < size; i++) orc_curand_init(seed_base + (uint64_t)i, &randoms[i]);
 }
 
+/* Advance `count` states by n draws each.  The v[5] recurrence of orc_curand is
+ * linear over GF(2), so n steps are one 160x160 bit matrix A^n (built by
+ * squaring; column j = A^n applied to unit state e_j, 5 words per column);
+ * d is a plain counter, d += n * 362437.  Equivalent to n orc_curand calls
+ * (tests/test_oracle.py checks it against the stepped loop).  Used to replay
+ * the reference's recorded frame sequence: every calculatePSO call consumes a
+ * fixed D + 3*D*I draws per particle, whatever the pose. */
+typedef struct { uint32_t col[160][5]; } orc_gf2;
+
+static void gf2_apply(const orc_gf2* m, const uint32_t in[5], uint32_t out[5])
+{
+    uint32_t r[5] = {0, 0, 0, 0, 0};
+    for (int j = 0; j < 160; j++)
+        if ((in[j >> 5] >> (j & 31)) & 1u)
+            for (int w = 0; w < 5; w++) r[w] ^= m->col[j][w];
+    memcpy(out, r, sizeof(r));
+}
+
+static void gf2_mul(const orc_gf2* a, const orc_gf2* b, orc_gf2* out) /* out = a * b */
+{
+    orc_gf2 t;
+    for (int j = 0; j < 160; j++) gf2_apply(a, b->col[j], t.col[j]);
+    *out = t;
+}
+
+void orc_skipahead(orc_rng* states, int64_t count, uint64_t n)
+{
+    orc_gf2* base = (orc_gf2*)malloc(sizeof(orc_gf2));
+    orc_gf2* acc = (orc_gf2*)malloc(sizeof(orc_gf2));
+    for (int j = 0; j < 160; j++) { /* base = A (one step), acc = identity */
+        orc_rng u;
+        memset(&u, 0, sizeof(u));
+        u.v[j >> 5] = 1u << (j & 31);
+        orc_curand(&u);
+        memcpy(base->col[j], u.v, sizeof(u.v));
+        memset(acc->col[j], 0, sizeof(acc->col[j]));
+        acc->col[j][j >> 5] = 1u << (j & 31);
+    }
+    for (uint64_t e = n; e; e >>= 1) {
+        if (e & 1u) gf2_mul(base, acc, acc);
+        if (e >> 1) gf2_mul(base, base, base);
+    }
+    const uint32_t dstep = (uint32_t)(n * 362437u);
+    for (int64_t i = 0; i < count; i++) {
+        gf2_apply(acc, states[i].v, states[i].v);
+        states[i].d += dstep;
+    }
+    free(base);
+    free(acc);
+}
+
 /* fill out[n] with uniforms drawn from one state (for RNG known-answer tests) */
 void orc_uniform_stream(orc_rng* s, float* out, int n)
 {

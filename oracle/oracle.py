@@ -76,6 +76,7 @@ def _bind(lib):
         "orc_curand_uniform": (ctypes.c_float, [_P]),
         "orc_init_generators": (None, [_P, ctypes.c_int64, ctypes.c_uint64]),
         "orc_uniform_stream": (None, [_P, _P, ctypes.c_int]),
+        "orc_skipahead": (None, [_P, ctypes.c_int64, ctypes.c_uint64]),
         "orc_chain_matrices": (None, [_P, ctypes.c_int, _P, _P]),
         "orc_fitness": (ctypes.c_float, [_P, ctypes.c_int, _P, _P, ctypes.c_float, ctypes.c_float]),
         "orc_fitness_ex": (ctypes.c_float, [_P, ctypes.c_int, _P, _P, ctypes.c_float, ctypes.c_float,
@@ -163,6 +164,14 @@ def uniform_stream(state: np.ndarray, n: int) -> np.ndarray:
     out = np.empty(n, dtype=np.float32)
     load().orc_uniform_stream(state.ctypes.data, _p(out), int(n))
     return out
+
+
+def skipahead(states: np.ndarray, n: int) -> np.ndarray:
+    """Advance every state by n draws in place (GF(2) jump; = n curand() calls)."""
+    st = np.ascontiguousarray(states)
+    assert st.dtype == RNG_DTYPE and st is states, "skipahead needs a contiguous RNG_DTYPE array"
+    load().orc_skipahead(st.ctypes.data, int(st.shape[0]), int(n))
+    return states
 
 
 def raw_stream(state: np.ndarray, n: int) -> np.ndarray:

@@ -49,3 +49,22 @@ def device():
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     return torch.device("cuda:0")
+
+
+@pytest.fixture(scope="session")
+def report():
+    """report(name, dict): with IKPSO_REPORT_DIR set, a test writes the measured
+    distribution behind its assertions to <dir>/<name>.json (committed under
+    profiles/ so the parity claims can be audited from the repo)."""
+    import json
+
+    out = os.environ.get("IKPSO_REPORT_DIR")
+
+    def write(name: str, data: dict) -> None:
+        print(f"[{name}] " + json.dumps(data, sort_keys=True)[:2000])
+        if out:
+            os.makedirs(out, exist_ok=True)
+            with open(os.path.join(out, name + ".json"), "w") as f:
+                json.dump(data, f, indent=1, sort_keys=True)
+
+    return write

@@ -536,3 +536,37 @@ def test_wide_angle_ranges_take_the_polynomial(oracle, device):
     assert np.max(np.abs(ang - oang)) < 1e-3, np.max(np.abs(ang - oang))  # ~16 ulp at 800 rad
     assert np.max(np.abs(fit - ofit) / ofit) < 1e-4, np.max(np.abs(fit - ofit) / ofit)
     assert np.max(np.abs(res - ores)) < 1e-3
+
+
+@pytest.mark.parametrize("variant", ["wide_bounds", "colliders"])
+def test_long_chain_collider_builds_plan_their_residency(oracle, device, variant):
+    """The collider builds (which also carry chains with angle ranges beyond
+    100 rad) run one cooperative workgroup per CU; the launch plan must count
+    that, not the two per CU of the plain long-chain build.  A 20-joint chain
+    with P = 16384 (64 chunks of 256) has no feasible cooperative plan at one
+    workgroup per CU, so AUTO takes the streaming kernels instead of launching
+    a group that cannot fit."""
+    wl = ikpso.workload(5)
+    chain = wl.chain.copy()
+    colliders = None
+    if variant == "wide_bounds":
+        chain["min_rotation"][1:] = -1000.0
+        chain["max_rotation"][1:] = 1000.0
+    else:
+        colliders = np.concatenate([ikpso.make_collider((0.5, 0.5, 0.5), (2.0, 0.0, 0.0)),
+                                    ikpso.make_collider((0.5, 0.5, 0.5), (0.0, 2.0, 0.0))])
+    B, P, I = 1, 16384, 2
+    tg = wl.targets(0, B)
+    s = ikpso.BatchSolver(chain, P, pso=ikpso.PSOConfig(0.5, 0.5, 1.25, I), limit_weight=wl.limit_weight,
+                          soft_lo=wl.soft_lo, soft_hi=wl.soft_hi, colliders=colliders)
+    s.seed(B)
+    ang, fit, res = (t.cpu().numpy() for t in s.solve(dev(tg), iterations=I))
+    kernel = s.kernel
+    s.close()
+    assert "streaming" in kernel, kernel
+    ostate = oracle.init_generators(B * P, 0)
+    oang, ofit, ores = oracle.solve_batch(chain, tg, None, P, I, ostate, limit_weight=wl.limit_weight,
+                                          soft_lo=wl.soft_lo, soft_hi=wl.soft_hi, colliders=colliders, threads=8)
+    assert np.all(np.isfinite(ang)) and np.all(np.isfinite(fit))
+    assert np.max(np.abs(fit - ofit) / ofit) < 1e-4, (fit, ofit)
+    assert np.max(np.abs(ang - oang)) < 1e-3
