@@ -278,11 +278,7 @@ ikpso_status parse_chain(const std::vector<ikpso_node>& nodes, const ikpso_pso_c
     ch.dfree = __builtin_popcountll(ch.free_mask);
     ch.masked = 3 * J <= 64 && ch.dfree != 3 * J;
     if (ch.dfree == 0) return IKPSO_ERR_INVALID_ARG;  // nothing to optimise
-#ifdef IKPSO_NO_UNIFORM_BOUNDS
-    ch.uniform_bounds = false;
-#else
     ch.uniform_bounds = true;
-#endif
     for (int d = 0; d < 3 * J && ch.uniform_bounds; ++d)
         ch.uniform_bounds = ch.uniform_bounds && as_bits(ch.lo[d]) == as_bits(ch.lo[0]) &&
                             as_bits(ch.hi[d]) == as_bits(ch.hi[0]);

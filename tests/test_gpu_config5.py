@@ -9,14 +9,16 @@ strict global-best improvement); SURVEY.md §8(c) tiers A and B.
 
   * REFERENCE arithmetic, 2 swarms x 4096 x I = 20: bit-exact angles, fitness
     and generator states (the draw count is integer work);
-  * FAST arithmetic, tier B, 32 swarms x 4096 x I = 500 (chaotic regime):
-    >= 80 % of swarms within |df|/f <= 1e-3 of the oracle and every swarm within
-    1e-2, median |df|/f <= 1e-4, mean fitness within 0.5 %, generator states
-    bit-exact.  The per-swarm bound is set by the dynamics, not by the kernel:
-    the oracle itself, built with and without FMA contraction (two valid fp32
-    evaluations one rounding apart), agrees within 1e-3 on 30 of 32 swarms of
-    this workload, median 4e-6, max 2.8e-3; the config-3 tier B
-    (21 angles, 1024 particles) keeps its 90 % bound;
+  * FAST arithmetic, tier B, 32 swarms x 4096 x I = 500 (chaotic regime), per
+    swarm against SURVEY.md §8(c)'s tolerances (|df|/f <= 1e-3, residual within
+    1e-3, tip position of the answer within 1e-2 through FK): >= 80 % of swarms
+    within each, every swarm within |df|/f <= 1e-2, |dr| <= 0.05, tip <= 0.05;
+    median |df|/f <= 1e-4, mean fitness within 0.5 %, generator states bit-exact.
+    The per-swarm bounds are the dynamics', not the kernel's: the oracle itself,
+    built with and without FMA contraction (two valid fp32 evaluations one
+    rounding apart), meets the tolerances on 94 / 91 / 94 % of these swarms,
+    worst 2.8e-3 / 1.3e-2 / 1.3e-2 (tools/tier_b_envelope.py,
+    profiles/r04/tier_b_envelope.json);
   * the cooperative solve's streaming fallback (and an explicit streaming solve)
     evaluate the tip from the tip back like the cooperative kernel, so FAST
     results agree across the families (I <= 10: |dtheta| <= 1e-3, |df|/f <= 1e-4).
@@ -25,6 +27,7 @@ import numpy as np
 import pytest
 
 import ikpso
+from tierb import tier_b_distances, tier_b_report
 
 pytestmark = pytest.mark.gpu
 
@@ -59,7 +62,7 @@ def oracle_batch(oracle, wl, B, I, threads=0):
     return tg, oang, ofit, ores, ostate
 
 
-def test_config5_reference_bitexact_g8(oracle, device):
+def test_config5_reference_bitexact_g16(oracle, device):
     """2 swarms x 4096 particles x 20 iterations through k_swarm_coop with G = 16."""
     B, I = 2, 20
     wl, s = config5_solver("reference", I)
@@ -77,7 +80,7 @@ def test_config5_reference_bitexact_g8(oracle, device):
     assert np.max(np.abs(res - ores)) <= 1e-5
 
 
-def test_config5_fast_tier_b_own_size(oracle, device):
+def test_config5_fast_tier_b_own_size(oracle, device, report):
     """32 swarms x 4096 particles x 500 iterations (the benchmarked kernel, FAST)."""
     B, I = 32, 500
     wl, s = config5_solver("fast", I)
@@ -95,8 +98,14 @@ def test_config5_fast_tier_b_own_size(oracle, device):
     print(f"tier B config 5: {frac:.3f} of {B} swarms within 1e-3; median |df|/f {np.median(rel):.2e}, "
           f"max {rel.max():.2e}; mean fitness {fit.mean():.6f} vs {ofit.mean():.6f}; "
           f"mean residual {res.mean():.5f} vs {ores.mean():.5f}")
+    rel, dres, dpos = tier_b_distances(wl.chain, ang, fit, res, oang, ofit, ores)
+    rep = tier_b_report(rel, dres, dpos)
+    rep.update(mean_fitness=float(fit.mean()), oracle_mean_fitness=float(ofit.mean()))
+    report("tier_b_config5", rep)
     assert frac >= 0.8, (frac, np.sort(rel)[-6:])
+    assert rep["frac_res_le_1e-3"] >= 0.8 and rep["frac_pos_le_1e-2"] >= 0.8, rep
     assert rel.max() <= 1e-2 and np.median(rel) <= 1e-4, (np.median(rel), rel.max())
+    assert dres.max() <= 0.05 and dpos.max() <= 0.05, rep
     assert abs(fit.mean() - ofit.mean()) / ofit.mean() < 5e-3
     assert abs(res.mean() - ores.mean()) < 1e-3 + 0.01 * ores.mean()
     # the reported fitness is the fitness of the reported angles (penalty included)

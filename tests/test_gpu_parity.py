@@ -16,6 +16,7 @@ import numpy as np
 import pytest
 
 import ikpso
+from tierb import tier_b_distances, tier_b_report
 
 pytestmark = pytest.mark.gpu
 
@@ -200,13 +201,19 @@ def tier_b_case(oracle):
 
 @pytest.mark.parametrize("kernel", ["resident", "auto"])
 @pytest.mark.parametrize("arith", ["fast", "reference"])
-def test_tier_b_config3_batch(oracle, device, tier_b_case, arith, kernel):
-    """Tier B: >= 90 % of the 64 swarms within |df|/f <= 1e-3 of the oracle's
-    gbest fitness, mean gbest fitness within 0.5 %, mean residual within 1e-3 +
-    1 %; the generator states after 500 iterations are bit-exact (draw count).
+def test_tier_b_config3_batch(oracle, device, tier_b_case, arith, kernel, report):
+    """Tier B on the benchmarked workload, 64 swarms x 1024 x 500, per swarm
+    (|df|/f <= 1e-3, residual within 1e-3, effector positions of
+    the answer within 1e-2 through FK).  After 500 chaotic iterations not every
+    swarm can meet those: two valid fp32 evaluations of the same solve -- the
+    oracle with and without FMA contraction -- meet them on 94 / 91 / 92 % of
+    these swarms, worst swarm 4.0e-2 / 1.4e-2 / 0.21 (tools/tier_b_envelope.py,
+    profiles/r04/tier_b_envelope.json).  So: >= 85 % of swarms within each
+    per-swarm tolerance (>= 90 % for the fitness), every swarm within 2.5x the
+    envelope's worst (|df|/f <= 0.1, |dr| <= 0.05, positions <= 0.5), mean gbest
+    fitness within 0.5 %; the generator states after 500 iterations bit-exact.
     REFERENCE arithmetic: every swarm bit-exact.  AUTO with 64 swarms runs the
-    cooperative latency variant (4 CUs per swarm: config 2's kernel) over the
-    same 64 swarms of 1024 x 500."""
+    cooperative latency variant (4 CUs per swarm: config 2's kernel)."""
     wl, tg, oang, ofit, ores, ostate = tier_b_case
     B, P, I = TIER_B_SWARMS, wl.particles, wl.iterations
     s = ikpso.BatchSolver(wl.chain, P, pso=wl.pso, arith=arith, kernel=kernel)
@@ -219,11 +226,13 @@ def test_tier_b_config3_batch(oracle, device, tier_b_case, arith, kernel):
     if arith == "reference":
         assert np.array_equal(ang, oang) and np.array_equal(fit, ofit)
         return
-    rel = np.abs(fit - ofit) / ofit
-    frac = float(np.mean(rel <= 1e-3))
-    print(f"tier B config 3: {frac:.3f} of {B} swarms within 1e-3; median |df|/f {np.median(rel):.2e}, "
-          f"max {rel.max():.2e}; mean fitness {fit.mean():.6f} vs {ofit.mean():.6f}")
-    assert frac >= 0.9, (frac, np.sort(rel)[-8:])
+    rel, dres, dpos = tier_b_distances(wl.chain, ang, fit, res, oang, ofit, ores)
+    rep = tier_b_report(rel, dres, dpos)
+    rep.update(mean_fitness=float(fit.mean()), oracle_mean_fitness=float(ofit.mean()), kernel=kernel)
+    report(f"tier_b_config3_{kernel}", rep)
+    assert rep["frac_rel_le_1e-3"] >= 0.9, (rep, np.sort(rel)[-8:])
+    assert rep["frac_res_le_1e-3"] >= 0.85 and rep["frac_pos_le_1e-2"] >= 0.85, rep
+    assert rel.max() <= 0.1 and dres.max() <= 0.05 and dpos.max() <= 0.5, rep
     assert abs(fit.mean() - ofit.mean()) / ofit.mean() < 5e-3
     assert abs(res.mean() - ores.mean()) < 1e-3 + 0.01 * ores.mean()
 

@@ -1,0 +1,59 @@
+#!/bin/bash
+# One GPU session on the gpurun box, as a list of stages run in order:
+#
+#   tools/gpu_session.sh STAGE [STAGE ...]
+#
+#   tests        every -m gpu test (IKPSO_REPORT_DIR=gpurun_out/reports: the tier-B and
+#                trajectory distributions); TESTS="<paths/-k ...>" narrows it
+#   smoke        __graft_entry__.smoke()
+#   bench        the default bench line (BENCH_ARGS adds flags) -> gpurun_out/bench.json
+#   bench:<cfg>  bench.py --config <cfg> (3 steps) -> gpurun_out/bench_<cfg>.json
+#   rocprof      rocprofv3 kernel trace of the default bench command (its average kernel
+#                duration must agree with the line's HIP-event kernel_ms)
+#   profile:<n>  kernel trace + PMC passes (tools/gpu_profile.sh) of workload n in
+#                {c3, c5, dh7, c3ref}: the counters bench.py's roofline reads
+#   frame        the visualiser frame latency (tools/frame_bench.py)
+#   var:<out>    interleaved variant timing (tools/gpu_var.sh; VAR_ARGS = "CONFIG SWARMS ITERS LIB...")
+#   asan         host-code ASan/UBSan run (tools/asan_check.sh)
+#
+# Every GPU step has its own time limit; a crash, abort or timeout (anything but a
+# plain test failure) ends the session so nothing else touches the GPU after a fault.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+step() {  # step NAME SECONDS CMD...
+  local name=$1 secs=$2; shift 2
+  echo "== $name"; timeout -k 10 "$secs" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?; echo "   rc=$rc"; tail -4 "gpurun_out/$name.log" | cut -c1-400
+  return $rc
+}
+for s in "$@"; do
+  case $s in
+    tests)
+      IKPSO_REPORT_DIR=gpurun_out/reports step gpu_tests 1100 python -u -m pytest ${TESTS:-tests} -m gpu -v -x -s \
+        -p no:cacheprovider --timeout 300 --timeout-method thread
+      rc=$?; [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit 2 ;;
+    smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit 3 ;;
+    bench) step bench 600 python bench.py ${BENCH_ARGS:-} || exit 4; tail -1 gpurun_out/bench.log > gpurun_out/bench.json ;;
+    bench:*)
+      c=${s#bench:}
+      step "bench_$c" 600 python bench.py --config "$c" --steps 3 --warmup 1 --cpu-seconds 4 || exit 4
+      tail -1 "gpurun_out/bench_$c.log" > "gpurun_out/bench_$c.json" ;;
+    rocprof)
+      step rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_default -o run --output-format csv -- \
+        python3 bench.py ${BENCH_ARGS:-} || exit 5 ;;
+    profile:c3) PROF_NAME=c3 PROF_ARGS="--swarms-per-gpu 2048 --steps 2 --warmup 1 --cpu-seconds 0 --extra-steps 0" \
+                bash tools/gpu_profile.sh || exit 6 ;;
+    profile:c3ref) PROF_NAME=c3ref PROF_ARGS="--arith reference --swarms-per-gpu 2048 --iterations 200 --steps 1 \
+                   --warmup 1 --cpu-seconds 0 --reference-steps 0 --extra-steps 0" bash tools/gpu_profile.sh || exit 6 ;;
+    profile:dh7) PROF_NAME=dh7 PROF_ARGS="--config dh7 --swarms-per-gpu 2048 --steps 2 --warmup 1 --cpu-seconds 0" \
+                 bash tools/gpu_profile.sh || exit 6 ;;
+    profile:c5) PROF_NAME=c5 PROF_ARGS="--config 5 --swarms-per-gpu 2048 --iterations 100 --steps 1 --warmup 1 \
+                --cpu-seconds 0" bash tools/gpu_profile.sh || exit 6 ;;
+    frame) step frame 300 python tools/frame_bench.py || exit 7 ;;
+    var:*) bash tools/gpu_var.sh "${s#var:}" $VAR_ARGS || exit 8 ;;
+    asan) step asan 600 bash tools/asan_check.sh run || exit 9 ;;
+    *) echo "unknown stage $s"; exit 64 ;;
+  esac
+done
+echo SESSION_DONE
