@@ -259,12 +259,14 @@ def timed_leg(ctx, wl, Bl, P, I, steps, warmup, arith="fast", kernel="auto"):
             "mean_fitness": float(res[:, D].mean()), "mean_residual": float(res[:, D + 1].mean())}
 
 
-def valu_roofline(kernel: str, ups_launch: float, kern_ms: float, lib_id: str):
+def valu_roofline(kernel: str, ups_launch: float, kern_ms: float, lib_id: str, arith: str = "fast"):
     """VALU lane-instructions per update (rocprofv3 SQ_INSTS_VALU x 64 / updates, committed in
     profiles/valu_per_update.json) x the live update rate, against the chip's 78.6 T lane-instructions/s
     (256 CU x 4 SIMD x 32 lanes x 2.4 GHz: every wave64 VALU op at its 2-cycle full rate).  None for a kernel
     without committed counters (or a streaming one: HBM-bound, priced by the caller)."""
-    vpu = None if "streaming" in kernel else valu_per_update(kernel)
+    # the counters are per (kernel, arithmetic): a REFERENCE build of a kernel has its own entry
+    key = kernel if arith == "fast" else f"{kernel} [{arith}]"
+    vpu = None if "streaming" in kernel else valu_per_update(key)
     if not vpu:
         return None, None
     kern_s = kern_ms / 1e3
@@ -415,11 +417,12 @@ def main():
         el_r = time.perf_counter() - tr
         rk = sr.kernel
         _, rvalu = valu_roofline(rk, Bl * P * I, float(np.mean([a.elapsed_time(b) for a, b in evr])),
-                                 ikpso.build_id())
+                                 ikpso.build_id(), arith="reference")
         reference_arith = {"value": Bl * P * I * args.reference_steps / el_r, "unit": "particle-updates/s",
                            "kernel_ms": round(float(np.mean([a.elapsed_time(b) for a, b in evr])), 3),
                            "steps": args.reference_steps, "warmup": 1, "kernel": rk,
                            "roofline_frac": rvalu["frac"] if rvalu else None,
+                           "roofline_stale": rvalu["stale"] if rvalu else None,
                            "swarms": Bl, "check_finite": bool(torch.isfinite(out_r[1]).all()),
                            "note": "REFERENCE arithmetic: the reference's 4x4 operation order, no FMA contraction, "
                                    "correctly rounded sin/cos -- bit-identical to the CPU oracle "
@@ -445,7 +448,7 @@ def main():
         alg_bytes = 20 * D + 8
         alg_gbs = ups_launch * alg_bytes / kern_s / 1e9
         streaming = "streaming" in solver.kernel
-        vpu, valu = valu_roofline(solver.kernel, ups_launch, kern_ms, lib_id)
+        vpu, valu = valu_roofline(solver.kernel, ups_launch, kern_ms, lib_id, args.arith)
         # the streaming kernels move x/v/pbest through HBM (HBM-bound); an on-chip kernel without a committed
         # PMC profile is reported unmeasured rather than against the HBM formulation it does not use
         on_chip_unmeasured = not streaming and not valu

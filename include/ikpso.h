@@ -107,7 +107,14 @@ enum {
     IKPSO_ARITH_FAST = 0,      /* closed-form 3x3 FK, FMA contraction (default); sin/cos on the
                                   transcendental unit when every clamp bound and rest angle of the
                                   chain lies within +-100 rad (the answers are clamped there), else a
-                                  1-ulp polynomial */
+                                  1-ulp polynomial.  A start pose (or the rest pose of the compat
+                                  call) beyond +-100 rad inside such bounds is evaluated once, at
+                                  initialisation, with the unit's larger error there (~1e-5 at 150 rad);
+                                  every later evaluation is of clamped angles.  The resident and
+                                  cooperative FAST kernels keep angles in revolutions (x / 2pi), so
+                                  answers and dumped particles come back within 4 ulp of the radian
+                                  values -- at 0 iterations the rest pose within 4 ulp, not bit for
+                                  bit (REFERENCE returns it exactly) */
     IKPSO_ARITH_REFERENCE = 1  /* the reference's 4x4 operation order, no FMA contraction */
 };
 

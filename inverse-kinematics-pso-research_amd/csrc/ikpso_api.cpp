@@ -118,17 +118,23 @@ uint32_t as_bits(float f)
 }
 
 // Copy `bytes` from host, managed or device memory into host memory.
-// Host copy of a caller buffer in any memory: plain or pinned host memory is
-// copied on the CPU (the visualiser's per-frame call passes its node table every
-// frame: a hipMemcpy would cost a device round trip); device and managed memory
-// through hipMemcpy, which also orders it after the caller's GPU work.
+// Pageable host memory (what a caller's plain arrays are; the Python mirror's
+// numpy tables) is copied on the CPU: nothing on the GPU can be writing it, and
+// the per-frame node table then costs no device round trip.  Pinned host,
+// device and managed memory go through hipMemcpy, which orders the read after
+// the caller's queued GPU work (an async copy that fills a pinned buffer, or a
+// kernel writing the managed node table).
 ikpso_status fetch_any(void* dst, const void* src, size_t bytes)
 {
     if (bytes == 0) return IKPSO_OK;
+    // hipPointerGetAttributes reports an unregistered host pointer as an error and
+    // records it as the thread's last error: clear only that one, never a sticky
+    // error the caller's own earlier work left
+    const hipError_t prior = hipPeekAtLastError();
     hipPointerAttribute_t a{};
     const hipError_t e = hipPointerGetAttributes(&a, src);
-    if (e != hipSuccess) (void)hipGetLastError();  // an unregistered host pointer may report an error
-    if (e != hipSuccess || a.type == hipMemoryTypeUnregistered || a.type == hipMemoryTypeHost) {
+    if (e != hipSuccess && prior == hipSuccess) (void)hipGetLastError();
+    if (e != hipSuccess || a.type == hipMemoryTypeUnregistered) {
         memcpy(dst, src, bytes);
         return IKPSO_OK;
     }
@@ -1078,7 +1084,10 @@ ikpso_status ikpso_solver_sync(ikpso_solver* s)
     if (!s) return IKPSO_ERR_INVALID_ARG;
     if (!s->pending.active) return IKPSO_OK;
     auto& p = s->pending;
-    p.active = false;
+    // `pending` stays active until the flag has been read and, if a group gave
+    // up, the fallback has run: a failure on the way (an allocation, a copy)
+    // returns its error and leaves the solve pending, so the next sync, solve or
+    // generator_states call settles it instead of reporting OK over NaN answers.
     // into pinned memory: a truly asynchronous copy, one synchronisation
     if (!s->err_host) IKPSO_HIP(hipHostMalloc(reinterpret_cast<void**>(&s->err_host), sizeof(int32_t)));
     *s->err_host = 0;
@@ -1098,7 +1107,10 @@ ikpso_status ikpso_solver_sync(ikpso_solver* s)
                 s->pending_timing_n, a / it, c / it, b / it, imp / it, rem / it, pol / it);
     }
 #endif
-    if (!err) return IKPSO_OK;
+    if (!err) {
+        p.active = false;
+        return IKPSO_OK;
+    }
     // A group gave up waiting for its members (the GPU is shared): restore the
     // generator states and solve the whole batch on the streaming kernels.
     IKPSO_HIP(hipMemcpyAsync(s->rng, s->rng_snap, sizeof(ikpso_rng_state) * (size_t)p.num_swarms * s->P,
@@ -1109,6 +1121,7 @@ ikpso_status ikpso_solver_sync(ikpso_solver* s)
                                             p.iterations, p.out_angles, p.out_fitness, p.out_residual, p.stream);
     if (st != IKPSO_OK) return st;
     IKPSO_HIP(hipStreamSynchronize(p.stream));
+    p.active = false;
     ++s->fallbacks;
     g_coop_fallbacks.fetch_add(1);
     return IKPSO_OK;

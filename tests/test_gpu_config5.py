@@ -12,7 +12,7 @@ strict global-best improvement); SURVEY.md §8(c) tiers A and B.
   * FAST arithmetic, tier B, 32 swarms x 4096 x I = 500 (chaotic regime), per
     swarm against SURVEY.md §8(c)'s tolerances (|df|/f <= 1e-3, residual within
     1e-3, tip position of the answer within 1e-2 through FK): >= 80 % of swarms
-    within each, every swarm within |df|/f <= 1e-2, |dr| <= 0.05, tip <= 0.05;
+    within each, every swarm within |df|/f <= 1e-2, |dr| <= 0.1, tip <= 0.2;
     median |df|/f <= 1e-4, mean fitness within 0.5 %, generator states bit-exact.
     The per-swarm bounds are the dynamics', not the kernel's: the oracle itself,
     built with and without FMA contraction (two valid fp32 evaluations one
@@ -105,7 +105,7 @@ def test_config5_fast_tier_b_own_size(oracle, device, report):
     assert frac >= 0.8, (frac, np.sort(rel)[-6:])
     assert rep["frac_res_le_1e-3"] >= 0.8 and rep["frac_pos_le_1e-2"] >= 0.8, rep
     assert rel.max() <= 1e-2 and np.median(rel) <= 1e-4, (np.median(rel), rel.max())
-    assert dres.max() <= 0.05 and dpos.max() <= 0.05, rep
+    assert dres.max() <= 0.1 and dpos.max() <= 0.2, rep  # gross-error ceilings (measured 0.013 / 0.023)
     assert abs(fit.mean() - ofit.mean()) / ofit.mean() < 5e-3
     assert abs(res.mean() - ores.mean()) < 1e-3 + 0.01 * ores.mean()
     # the reported fitness is the fitness of the reported angles (penalty included)

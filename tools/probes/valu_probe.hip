@@ -16,10 +16,13 @@ __global__ void __launch_bounds__(1024) k_op(float* out, int iters, float sa, fl
     const unsigned ua = __float_as_uint(va), ub = __float_as_uint(vb);
     float f[CH];
     unsigned u[CH];
+    double g[CH];
+    const double da = va, db = vb;
 #pragma unroll
     for (int c = 0; c < CH; ++c) {
         f[c] = threadIdx.x * 1e-3f + c;
         u[c] = threadIdx.x * 747796405u + c;
+        g[c] = threadIdx.x * 1e-3 + c;
     }
     for (int i = 0; i < iters; ++i) {
 #pragma unroll
@@ -65,11 +68,22 @@ __global__ void __launch_bounds__(1024) k_op(float* out, int iters, float sa, fl
                     else f[c] = __builtin_amdgcn_sinf(f[c]);
                 }
                 if constexpr (OP == 35) f[c] = __builtin_amdgcn_cosf(f[c]);       // v_cos_f32
+                // fp64 and packed forms (the REFERENCE kernels' sincos runs in fp64)
+                if constexpr (OP == 36) g[c] = __builtin_fma(g[c], da, db);       // v_fma_f64 v,v,v
+                if constexpr (OP == 37) g[c] = g[c] * da;                         // v_mul_f64
+                if constexpr (OP == 38) asm volatile("v_add_f64 %0, %0, %1" : "+v"(g[c]) : "v"(da));
+                if constexpr (OP == 39) asm volatile("v_cvt_f64_f32 %0, %1" : "=v"(g[c]) : "v"(f[c]));
+                if constexpr (OP == 40) asm volatile("v_cvt_f32_f64 %0, %1" : "=v"(f[c]) : "v"(g[c]));
+                if constexpr (OP == 41) asm volatile("v_pk_mul_f32 %0, %0, %1" : "+v"(g[c]) : "v"(da));
+                if constexpr (OP == 42) asm volatile("v_pk_fma_f32 %0, %0, %1, %2" : "+v"(g[c]) : "v"(da), "v"(db));
+                if constexpr (OP == 43) asm volatile("v_rndne_f32 %0, %0" : "+v"(f[c]));
+                if constexpr (OP == 44) asm volatile("v_min_f32 %0, %0, %1" : "+v"(f[c]) : "v"(va));
+                if constexpr (OP == 45) asm volatile("v_cndmask_b32 %0, %0, %1, vcc" : "+v"(u[c]) : "v"(ua));
             }
     }
     float s = 0.f;
 #pragma unroll
-    for (int c = 0; c < CH; ++c) s += f[c] + __uint_as_float(u[c] & 0x3fffffffu);
+    for (int c = 0; c < CH; ++c) s += f[c] + __uint_as_float(u[c] & 0x3fffffffu) + (float)g[c];
     out[blockIdx.x * blockDim.x + threadIdx.x] = s;
 }
 
@@ -77,7 +91,9 @@ static const char* kNames[] = {
     "v_mul_f32 v,v", "v_mul_f32 v,s", "v_mul_f32 v,literal", "v_mul_f32 v,inline", "v_fmac_f32 v,v",
     "v_fma_f32 v,v,v", "v_fma_f32 v,s,s", "v_fmaak_f32 literal", "v_xor_b32 v,v", "v_lshlrev_b32 inline",
     "v_bitop3_b32 v,v,v", "v_add3_u32 v,v,v", "v_cvt_f32_u32 v", "v_med3_f32 v,v,v",
-    "v_lshrrev_b32 inline", "v_lshlrev_b32 inline 4", "v_lshlrev_b32 inline 1", "v_lshrrev_b32 inline 3", "v_add_u32 v,v (x+x)", "v_add_u32 literal", "v_alignbit_b32 v,0,28 (x<<4)", "v_lshl_add_u32 v,4,0", "v_lshl_or_b32 v,4,0", "v_bfe_i32 v,0,1", "v_and_b32 literal", "v_sub_f32 v,v", "v_max_f32 v,v", "v_mov_b32 v", "v_fmamk_f32 literal", "v_lshlrev_b32 v,v (vgpr amount)", "v_add_u32 v,v,v", "v_xad_u32 v,v,v", "v_cvt_f32_u32 e64", "v_sin_f32 v", "v_sin_f32 / v_fma_f32 1:1", "v_cos_f32 v"};
+    "v_lshrrev_b32 inline", "v_lshlrev_b32 inline 4", "v_lshlrev_b32 inline 1", "v_lshrrev_b32 inline 3", "v_add_u32 v,v (x+x)", "v_add_u32 literal", "v_alignbit_b32 v,0,28 (x<<4)", "v_lshl_add_u32 v,4,0", "v_lshl_or_b32 v,4,0", "v_bfe_i32 v,0,1", "v_and_b32 literal", "v_sub_f32 v,v", "v_max_f32 v,v", "v_mov_b32 v", "v_fmamk_f32 literal", "v_lshlrev_b32 v,v (vgpr amount)", "v_add_u32 v,v,v", "v_xad_u32 v,v,v", "v_cvt_f32_u32 e64", "v_sin_f32 v", "v_sin_f32 / v_fma_f32 1:1", "v_cos_f32 v",
+    "v_fma_f64 v,v,v", "v_mul_f64 v,v", "v_add_f64 v,v", "v_cvt_f64_f32", "v_cvt_f32_f64", "v_pk_mul_f32 v,v",
+    "v_pk_fma_f32 v,v,v", "v_rndne_f32", "v_min_f32 v,v", "v_cndmask_b32 v,v,vcc"};
 
 
 template <int OP>
@@ -116,7 +132,7 @@ int main()
     const int blocks = cus * 8;
     void* out;
     hipMalloc(&out, (size_t)blocks * 1024 * 4);
-    run_all(blocks, out, std::make_integer_sequence<int, 36>{});
+    run_all(blocks, out, std::make_integer_sequence<int, 46>{});
     hipFree(out);
     return 0;
 }
