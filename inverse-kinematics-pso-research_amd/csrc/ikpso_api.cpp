@@ -293,6 +293,8 @@ ikpso_status parse_chain(const std::vector<ikpso_node>& nodes, const ikpso_pso_c
         volatile float inv = 0.159154943091895336f;  // (no contraction or constant folding differences)
         const float rlo = ch.lo[0] * inv, rhi = ch.hi[0] * inv;
         ch.unit_rev_bounds = ch.uniform_bounds && rlo == 0.0f && rhi == 1.0f;
+        ch.ordered_bounds = ch.uniform_bounds && std::isfinite(ch.lo[0]) && std::isfinite(ch.hi[0]) &&
+                            ch.lo[0] <= ch.hi[0];
     }
     ref7 = ref7 && eff_mask == 0xE0ull;                // effectors = nodes 5, 6, 7
     serial = serial && eff_mask == (1ull << J);        // single tip effector

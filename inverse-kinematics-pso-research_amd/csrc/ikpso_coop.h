@@ -248,6 +248,13 @@ __global__ void __launch_bounds__(BLOCK, (kCoopMinWaves<Topo::D, BLOCK, TERMS>))
     }
     __syncthreads();
     const PsoCoef coef = pso_coef(cc);
+#if IKPSO_COOP_STAGGER > 0
+    // Experiment: start the second half of the grid (the second workgroup of each
+    // CU in dispatch order) IKPSO_COOP_STAGGER x 64 cycles late, so the two swarms
+    // sharing a CU begin out of phase (one's hand-off under the other's step).
+    if (kCoopMinWaves<D, BLOCK, TERMS> > (BLOCK >= 256 ? BLOCK / 256 : 1) && blockIdx.x >= gridDim.x / 2)
+        for (int s = 0; s < IKPSO_COOP_STAGGER; s += 64) __builtin_amdgcn_s_sleep(64);
+#endif
 
     for (;;) {
         compiler_fence();

@@ -197,8 +197,52 @@ __host__ __device__ __forceinline__ void sincos_fast(float x, float* s_out, floa
 // the correctly rounded sinf/cosf except in vanishingly rare near-tie cases --
 // the same property the host libm's double-evaluated sinf/cosf has, which
 // keeps this mode in bitwise agreement with the CPU oracle.
+#ifndef IKPSO_REF_SINCOS_LEAN
+#define IKPSO_REF_SINCOS_LEAN 1
+#endif
 __host__ __device__ __forceinline__ void sincos_reference(float x, float* s_out, float* c_out)
 {
+#if IKPSO_REF_SINCOS_LEAN
+    // The quadrant by the fp64 round-to-integer magic constant (k = rint(x*2/pi):
+    // one fma and one add instead of a multiply, a rint and two conversions), the
+    // quadrant's swap and signs as bit selects on the fp32 results (bitop3 / xor
+    // instead of compares and cndmasks).  Near a quadrant boundary k may differ by
+    // one from the fp32 rint's; the reduced argument then lies just past pi/4,
+    // where the polynomials are as accurate, so the rounded result is the same.
+    const double xd = (double)x;
+    const double kb = __builtin_fma(xd, 6.36619772367581382433e-01, 6755399441055744.0);  // 1.5 * 2^52 + k
+    const double k = kb - 6755399441055744.0;
+    uint64_t kbits;
+    __builtin_memcpy(&kbits, &kb, 8);
+    const uint32_t q = (uint32_t)kbits;  // k mod 2^32 (two's complement)
+    double r = __builtin_fma(-k, 1.57079632673412561417e+00, xd);
+    r = __builtin_fma(-k, 6.07710050650619224932e-11, r);
+    const double z = r * r;
+    double sp = __builtin_fma(z, 1.58969099521155010221e-10, -2.50507602534068634195e-08);
+    sp = __builtin_fma(z, sp, 2.75573137070700676789e-06);
+    sp = __builtin_fma(z, sp, -1.98412698298579493134e-04);
+    sp = __builtin_fma(z, sp, 8.33333333332248946124e-03);
+    sp = __builtin_fma(z, sp, -1.66666666666666324348e-01);
+    const double sv = __builtin_fma(r * z, sp, r);
+    double cp = __builtin_fma(z, -1.13596475577881948265e-11, 2.08757232129817482790e-09);
+    cp = __builtin_fma(z, cp, -2.75573143513906633035e-07);
+    cp = __builtin_fma(z, cp, 2.48015872894767294178e-05);
+    cp = __builtin_fma(z, cp, -1.38888888888741095749e-03);
+    cp = __builtin_fma(z, cp, 4.16666666666666019037e-02);
+    const double cv = __builtin_fma(z * z, cp, __builtin_fma(-0.5, z, 1.0));
+    const uint32_t sf = as_uint((float)sv), cf = as_uint((float)cv);
+    const uint32_t m = 0u - (q & 1u);  // q odd: all ones (swap)
+#if defined(__HIP_DEVICE_COMPILE__)
+    const uint32_t s1 = __builtin_amdgcn_bitop3_b32(m, cf, sf, 0xCA);  // m ? cf : sf
+    const uint32_t c1 = __builtin_amdgcn_bitop3_b32(m, sf, cf, 0xCA);  // m ? sf : cf
+#else
+    const uint32_t s1 = (m & cf) | (~m & sf);
+    const uint32_t c1 = (m & sf) | (~m & cf);
+#endif
+    const uint32_t t = q << 30;  // bit 31: q & 2 (sin sign); (q + 1) & 2 for cos
+    *s_out = as_float(xor_sign(s1, t));
+    *c_out = as_float(xor_sign(c1, t + 0x40000000u));
+#else
     const float kf = __builtin_rintf(x * 0.636619772367581343f);
     const double k = (double)kf;
     double r = __builtin_fma(-k, 1.57079632673412561417e+00, (double)x);
@@ -224,6 +268,7 @@ __host__ __device__ __forceinline__ void sincos_reference(float x, float* s_out,
     cs = ((q + 1) & 2) ? -cs : cs;
     *s_out = sn;
     *c_out = cs;
+#endif
 }
 
 // ------------------------------------------------------------- topologies
@@ -1143,11 +1188,14 @@ __device__ __forceinline__ void pso_update_ahead(float& x, float& v, float g, fl
 __device__ __forceinline__ float clamp_ref(float v, float lo, float hi) { return fminf(fmaxf(v, lo), hi); }
 
 // FAST mode: one v_med3_f32 (the median of v, lo, hi is the clamp for lo <= hi
-// and finite v); REFERENCE mode keeps the reference's fmaxf/fminf pair.
-template <int MODE>
+// and finite v); REFERENCE mode keeps the reference's fmaxf/fminf pair, except
+// in its uniform-bounds builds (BOUNDS_ORDERED: the host dispatches them only for
+// finite lo <= hi, where the median is bit-identical to fminf(fmaxf(v, lo), hi)
+// for every non-NaN v -- one half-rate op instead of two).
+template <int MODE, bool BOUNDS_ORDERED = false>
 __device__ __forceinline__ float clamp_mode(float v, float lo, float hi)
 {
-    if constexpr (MODE == IKPSO_ARITH_FAST) return __builtin_amdgcn_fmed3f(v, lo, hi);
+    if constexpr (MODE == IKPSO_ARITH_FAST || BOUNDS_ORDERED) return __builtin_amdgcn_fmed3f(v, lo, hi);
     return clamp_ref(v, lo, hi);
 }
 

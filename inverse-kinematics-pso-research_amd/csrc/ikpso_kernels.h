@@ -60,6 +60,7 @@ struct ChainHost {
     bool use_posref = false, use_penalty = false;
     bool uniform_bounds = false;  // every angle has clamp bounds lo[0], hi[0]
     bool unit_rev_bounds = false; // ... and they are [0, 1] in revolutions (kTermUnitBounds): [0, 2pi]
+    bool ordered_bounds = false;  // ... and finite with lo <= hi (REFERENCE uniform builds: median clamp)
     bool sym_penalty = false;     // soft limits symmetric and within a revolution of the clamp (kTermSymPenalty)
     int num_coll = 0;             // colliders (obj_t) of the scene
     size_t coll_off = 0;          // float offset of the collider records in aux
@@ -115,6 +116,17 @@ __host__ __device__ constexpr int kCoopBlocksPerCU()
 
 #ifndef IKPSO_COOP_TIMING
 #define IKPSO_COOP_TIMING 0  // measurement builds: per-workgroup cycles in the step and in the hand-off
+#endif
+// Experiment (A/B timing): sleep units of 64 cycles the second workgroup of each CU
+// waits before its first swarm (k_swarm_coop, two workgroups per CU); 0: none.
+#ifndef IKPSO_COOP_STAGGER
+#define IKPSO_COOP_STAGGER 0
+#endif
+// REFERENCE arithmetic on the reference scene with uniform ordered bounds gets its
+// own resident build (no runtime term tests, median clamp); 0: the runtime-term
+// build as before (A/B timing).
+#ifndef IKPSO_REF_UNIFORM_BUILD
+#define IKPSO_REF_UNIFORM_BUILD 1
 #endif
 // The cooperative latency variant with its generators on separate waves
 // (k_swarm_coop_split, ikpso_coop.h); 0 builds the unsplit one (A/B timing).

@@ -80,7 +80,7 @@ __device__ __forceinline__ void update_node(const ChainConsts<Topo::J>& cc, cons
         if (kMasked<Topo, TERMS> && !dim_free(cc, d)) continue;  // locked: stays at rest
         pso_update<MODE>(x[d], v[d], s_pb[d * BLOCK + tid], sh.g[d], coef, rng);
         if constexpr (TERMS & kTermUniformBounds)
-            x[d] = clamp_mode<MODE>(x[d], uniform_lo<TERMS>(cc), uniform_hi<TERMS>(cc));
+            x[d] = clamp_mode<MODE, true>(x[d], uniform_lo<TERMS>(cc), uniform_hi<TERMS>(cc));
         else
             x[d] = clamp_mode<MODE>(x[d], sh.lo[d], sh.hi[d]);
     }
@@ -170,7 +170,7 @@ __device__ __forceinline__ void swarm_step_tip(const ChainConsts<Topo::J>& cc, S
             else
                 pso_update<MODE>(x[d], v[d], cpb[ax], cg[ax], coef, rng);
             if constexpr (TERMS & kTermUniformBounds)
-                x[d] = clamp_mode<MODE>(x[d], uniform_lo<TERMS>(cc), uniform_hi<TERMS>(cc));
+                x[d] = clamp_mode<MODE, true>(x[d], uniform_lo<TERMS>(cc), uniform_hi<TERMS>(cc));
             else
                 x[d] = clamp_mode<MODE>(x[d], sh.lo[d], sh.hi[d]);
         }
@@ -262,7 +262,7 @@ __device__ __forceinline__ void swarm_step(const ChainConsts<Topo::J>& cc, Swarm
             if (MASK && !dim_free(cc, d)) continue;  // locked: stays at rest
             pso_update<MODE>(x[d], v[d], cpb[ax], cg[ax], coef, rng);
             if constexpr (TERMS & kTermUniformBounds)
-                x[d] = clamp_mode<MODE>(x[d], uniform_lo<TERMS>(cc), uniform_hi<TERMS>(cc));
+                x[d] = clamp_mode<MODE, true>(x[d], uniform_lo<TERMS>(cc), uniform_hi<TERMS>(cc));
             else
                 x[d] = clamp_mode<MODE>(x[d], sh.lo[d], sh.hi[d]);
         }
@@ -489,6 +489,14 @@ inline hipError_t run_resident(const ChainHost& ch, const SwarmIO& io, int block
         if (terms == (kTermUniformBounds | kTermPenalty)) {
             hipLaunchKernelGGL((k_swarm_resident<Topo, MODE, kTermUniformBounds | kTermPenalty | kTermRev>), grid,
                                threads, 0, stream, cc, io);
+            return hipGetLastError();
+        }
+    }
+    // REFERENCE on the reference scene (the bit-exact path the bench's reference_arith leg and the
+    // recorded-trajectory replay run): no runtime term tests, the median clamp for ordered bounds
+    if constexpr (std::is_same_v<Topo, TopoRef7> && MODE == IKPSO_ARITH_REFERENCE && IKPSO_REF_UNIFORM_BUILD) {
+        if (terms == kTermUniformBounds && ch.ordered_bounds) {
+            hipLaunchKernelGGL((k_swarm_resident<Topo, MODE, kTermUniformBounds>), grid, threads, 0, stream, cc, io);
             return hipGetLastError();
         }
     }

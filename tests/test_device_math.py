@@ -34,18 +34,35 @@ int main() {
     if (fabsf(tc) < 1e-3f) v = fabsf(cf - tc) < 1e-7f ? 0 : v;
     int m = u > v ? u : v; if (m > fast_max) fast_max = m; if (m) fast_off++;
   }
+  // REFERENCE near the quadrant boundaries k*pi/4 (where the fp64 and fp32 roundings of
+  // x*2/pi may pick different k): 64 neighbouring floats on each side of every boundary
+  for (int q = -40; q <= 40; q++) {
+    const float c = (float)(q * 0.78539816339744830962);
+    for (int side = 0; side < 2; side++) {
+      float x = c;
+      for (int j = 0; j < 64; j++, x = nextafterf(x, side ? 1e9f : -1e9f)) {
+        float sr, cr;
+        ikpso::sincos_reference(x, &sr, &cr);
+        if (sr != (float)sin((double)x) || cr != (float)cos((double)x)) ref_bad++;
+      }
+    }
+  }
   printf("%ld %d %ld %ld\n", ref_bad, fast_max, fast_off, n);
   return 0;
 }
 '''
 
 
-def test_device_sincos_on_host():
+@pytest.mark.parametrize("lean", [0, 1])
+def test_device_sincos_on_host(lean):
+    """lean: the REFERENCE sincos with the fp64 magic-constant quadrant and bit-select
+    fix-up (IKPSO_REF_SINCOS_LEAN)."""
     with tempfile.TemporaryDirectory() as td:
         src = Path(td) / "p.cpp"
         exe = Path(td) / "p"
         src.write_text(PROBE)
-        subprocess.run(["/opt/rocm/bin/hipcc", "-O2", "-std=c++17", "-ffp-contract=off", f"-I{CSRC}",
+        subprocess.run(["/opt/rocm/bin/hipcc", "-O2", "-std=c++17", "-ffp-contract=off", f"-DIKPSO_REF_SINCOS_LEAN={lean}",
+                        f"-I{CSRC}",
                         f"-I{ROOT / 'include'}", str(src), "-o", str(exe)], check=True, capture_output=True)
         ref_bad, fast_max, fast_off, n = map(int, subprocess.run([str(exe)], capture_output=True, text=True,
                                                                  check=True).stdout.split())
