@@ -1134,6 +1134,31 @@ struct Prescaled : std::false_type {};
 template <class Rng>
 struct Prescaled<Rng, std::void_t<decltype(Rng::kPrescaled)>> : std::bool_constant<Rng::kPrescaled> {};
 
+// v = a * v + c computed into v's own register.  Left to the compiler, the FMA
+// becomes a v_fmac that accumulates into c's register, so every velocity moves to
+// another register each iteration and the loop's back edge pays one v_mov per
+// dimension to restore the assignment (21 per wave-iteration in config 3's loop,
+// 58 in config 5's).  The tied asm operand keeps the register.
+#ifndef IKPSO_INPLACE_V
+#define IKPSO_INPLACE_V 1
+#endif
+__device__ __forceinline__ void fma_into(float& v, float a, float b, float c)  // v = a * b + c
+{
+#if defined(__HIP_DEVICE_COMPILE__) && IKPSO_INPLACE_V
+    asm("v_fma_f32 %0, %1, %2, %3" : "+v"(v) : "v"(a), "v"(b), "v"(c));
+#else
+    v = __builtin_fmaf(a, b, c);
+#endif
+}
+__device__ __forceinline__ void fma_inplace(float& v, float a, float c)  // v = a * v + c
+{
+#if defined(__HIP_DEVICE_COMPILE__) && IKPSO_INPLACE_V
+    asm("v_fma_f32 %0, %1, %0, %2" : "+v"(v) : "v"(a), "v"(c));
+#else
+    v = __builtin_fmaf(a, v, c);
+#endif
+}
+
 template <int MODE, class Rng>
 __device__ __forceinline__ void pso_update(float& x, float& v, float pb, float g, const PsoCoef& k, Rng& rng)
 {
@@ -1160,7 +1185,7 @@ __device__ __forceinline__ void pso_update(float& x, float& v, float pb, float g
         const float a = rng.scaled(k.wq, k.wh);
         const float b = rng.scaled(k.c1q, k.c1h);
         const float c = rng.scaled(k.c2q, k.c2h);
-        v = __builtin_fmaf(a, v, __builtin_fmaf(b, pb - x, c * (g - x)));
+        fma_inplace(v, a, __builtin_fmaf(b, pb - x, c * (g - x)));
         x += v;
     }
 }
@@ -1180,7 +1205,7 @@ __device__ __forceinline__ void pso_draw_ahead(float& pa, float& pc, float x, fl
 }
 __device__ __forceinline__ void pso_update_ahead(float& x, float& v, float g, float pa, float pc)
 {
-    v = __builtin_fmaf(pc, g - x, pa);
+    fma_into(v, pc, g - x, pa);
     x += v;
 }
 

@@ -8,6 +8,8 @@
 #   smoke        __graft_entry__.smoke()
 #   bench        the default bench line (BENCH_ARGS adds flags) -> gpurun_out/bench.json
 #   bench:<cfg>  bench.py --config <cfg> (3 steps) -> gpurun_out/bench_<cfg>.json
+#   gloo2        the N = 2 path rehearsed on the one GPU (two ranks over gloo sharing it; not a
+#                measurement): the default line with its config-4 leg at 2 x 8192 targets
 #   rocprof      rocprofv3 kernel trace of the default bench command (its average kernel
 #                duration must agree with the line's HIP-event kernel_ms)
 #   profile:<n>  kernel trace + PMC passes (tools/gpu_profile.sh) of workload n in
@@ -39,6 +41,9 @@ for s in "$@"; do
       c=${s#bench:}
       step "bench_$c" 600 python bench.py --config "$c" --steps 3 --warmup 1 --cpu-seconds 4 || exit 4
       tail -1 "gpurun_out/bench_$c.log" > "gpurun_out/bench_$c.json" ;;
+    gloo2)
+      step gloo2 600 python bench.py --gpus 2 --dist-backend gloo --steps 3 --warmup 1 --cpu-seconds 0 || exit 4
+      grep '^{' gpurun_out/gloo2.log | tail -1 > gpurun_out/bench_gloo2.json ;;
     rocprof)
       step rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_default -o run --output-format csv -- \
         python3 bench.py ${BENCH_ARGS:-} || exit 5 ;;
