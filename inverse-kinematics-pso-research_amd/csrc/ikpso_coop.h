@@ -203,8 +203,11 @@ __device__ __forceinline__ void coop_exchange(SwarmShared<Topo>& sh, CoopShared<
 // x 4096 x 100: 3 dimensions (node 1) 64.4 -> 63.3 ms; 6 and 9 measured no
 // better than 3 (the extra live values cost the step more than the window saves:
 // profiles/r03b, r03c variant_timings).
+#ifndef IKPSO_COOP_AHEAD_DIMS
+#define IKPSO_COOP_AHEAD_DIMS 3
+#endif
 template <class Topo, int MODE, int TERMS, int BLOCK>
-constexpr int kCoopAhead = (kTipBackward<Topo, MODE, TERMS> && Topo::D > 30) ? 3 : 0;
+constexpr int kCoopAhead = (kTipBackward<Topo, MODE, TERMS> && Topo::D > 30) ? IKPSO_COOP_AHEAD_DIMS : 0;
 // Waves per SIMD a cooperative build is compiled for: its own (BLOCK / 256)
 // times the workgroups that share a CU (the latency variant: 1, alone on its
 // CU).  The long chains' collider builds need more than 256 VGPRs: compiled for

@@ -1138,7 +1138,11 @@ struct Prescaled<Rng, std::void_t<decltype(Rng::kPrescaled)>> : std::bool_consta
 // becomes a v_fmac that accumulates into c's register, so every velocity moves to
 // another register each iteration and the loop's back edge pays one v_mov per
 // dimension to restore the assignment (21 per wave-iteration in config 3's loop,
-// 58 in config 5's).  The tied asm operand keeps the register.
+// 58 in config 5's, where the extra live copies also spilled).  The tied asm
+// operand keeps the register.  Used by the tip-backward step (config 5: -2.6 %,
+// the DH arm: -1.3 %); the software-pipelined 4-wave step keeps the compiler's
+// form -- there the opaque asm costs its scheduler more than the moves (config 3
+// +2 %; profiles/r04/variant_timings).
 #ifndef IKPSO_INPLACE_V
 #define IKPSO_INPLACE_V 1
 #endif
@@ -1159,7 +1163,7 @@ __device__ __forceinline__ void fma_inplace(float& v, float a, float c)  // v = 
 #endif
 }
 
-template <int MODE, class Rng>
+template <int MODE, bool INPLACE = false, class Rng>
 __device__ __forceinline__ void pso_update(float& x, float& v, float pb, float g, const PsoCoef& k, Rng& rng)
 {
     if constexpr (MODE == IKPSO_ARITH_REFERENCE && Prescaled<Rng>::value) {
@@ -1185,7 +1189,10 @@ __device__ __forceinline__ void pso_update(float& x, float& v, float pb, float g
         const float a = rng.scaled(k.wq, k.wh);
         const float b = rng.scaled(k.c1q, k.c1h);
         const float c = rng.scaled(k.c2q, k.c2h);
-        fma_inplace(v, a, __builtin_fmaf(b, pb - x, c * (g - x)));
+        if constexpr (INPLACE)
+            fma_inplace(v, a, __builtin_fmaf(b, pb - x, c * (g - x)));
+        else
+            v = __builtin_fmaf(a, v, __builtin_fmaf(b, pb - x, c * (g - x)));
         x += v;
     }
 }

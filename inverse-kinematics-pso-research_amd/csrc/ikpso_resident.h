@@ -32,7 +32,10 @@ constexpr int kTrigAheadMaxD = 30;
 // 4 / 3 / 2 / none 61.2 / 60.2 / 61.9 / 67.2 ms (profiles/r03s); config 3 48.3
 // -> 47.3 ms with 2 levels, 51.7 ms with 4 (profiles/r02g); the folded DH arm's
 // 4-wave tip-backward step unchanged within noise (so none).
-constexpr int kPrioLevels2Wave = 3, kPrioLevels4Wave = 2;
+#ifndef IKPSO_PRIO_LEVELS_2WAVE
+#define IKPSO_PRIO_LEVELS_2WAVE 3
+#endif
+constexpr int kPrioLevels2Wave = IKPSO_PRIO_LEVELS_2WAVE, kPrioLevels4Wave = 2;
 
 // Progress-levelled wave priority: entering node k of J a wave sets its issue
 // priority to (L-1) - L(k-1)/J, so a wave that has run ahead of the others on
@@ -168,7 +171,7 @@ __device__ __forceinline__ void swarm_step_tip(const ChainConsts<Topo::J>& cc, S
             if (d < KA)  // drawn ahead during the previous exchange (k_swarm_coop)
                 pso_update_ahead(x[d], v[d], cg[ax], pa[d], pc[d]);
             else
-                pso_update<MODE>(x[d], v[d], cpb[ax], cg[ax], coef, rng);
+                pso_update<MODE, true>(x[d], v[d], cpb[ax], cg[ax], coef, rng);
             if constexpr (TERMS & kTermUniformBounds)
                 x[d] = clamp_mode<MODE, true>(x[d], uniform_lo<TERMS>(cc), uniform_hi<TERMS>(cc));
             else

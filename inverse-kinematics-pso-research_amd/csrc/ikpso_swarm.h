@@ -116,13 +116,21 @@ __device__ __forceinline__ float radians(float a)
 
 // The swarm's answer over the free dimensions: out[b][dfree] from the kernel's
 // D-vector g (every thread of the calling workgroup; lanes < D write).
-// kTermRev builds: g in revolutions, scaled back to radians and held inside the
-// clamp bounds (a bound's round trip through revolutions may land an ulp out).
+// kTermRev builds: g in revolutions, scaled back to radians; an answer that lies
+// inside the clamp bounds (in the staged revolution bounds, lo * 1/2pi .. hi * 1/2pi)
+// is held inside them in radians too (a bound's round trip through revolutions may
+// land an ulp out).  An answer outside them -- the start pose itself, which the
+// reference never clamps (src/kernel.cu:223-266), winning every iteration -- is
+// returned as it is, as the reference returns it.
 template <class Topo, int TERMS = 0>
 __device__ __forceinline__ void store_angles(const ChainConsts<Topo::J>& cc, float* out, int64_t b, int d, float g)
 {
     if (d < Topo::D && dim_free(cc, d)) {
-        if constexpr (TERMS & kTermRev) g = fminf(fmaxf(g * k2Pi, cc.lo[d]), cc.hi[d]);
+        if constexpr (TERMS & kTermRev) {
+            const bool inside = g >= cc.lo[d] * kInv2Pi && g <= cc.hi[d] * kInv2Pi;
+            g *= k2Pi;
+            if (inside) g = fminf(fmaxf(g, cc.lo[d]), cc.hi[d]);
+        }
         out[b * cc.dfree + dim_rank(cc, d)] = g;
     }
 }

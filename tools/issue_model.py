@@ -18,6 +18,10 @@ COST4 = ("v_lshlrev_b32", "v_add3_u32", "v_cvt_f32_u32", "v_cvt_f32_i32", "v_cvt
          "v_mad_u64_u32", "v_mul_lo_u32", "v_mul_hi_u32", "v_readlane_b32", "v_writelane_b32", "v_perm_b32",
          "v_and_or_b32", "v_or3_b32", "v_cndmask_b32")
 TRANS = ("v_sin_f32", "v_cos_f32", "v_exp_f32", "v_log_f32", "v_rcp_f32", "v_rsq_f32", "v_sqrt_f32")
+# fp64 and packed-fp32 forms (round 4, profiles/r04/valu_issue_costs.txt): the REFERENCE sincos runs in fp64
+COSTF64 = {"v_fma_f64": 4.79, "v_fmac_f64": 4.79, "v_mul_f64": 4.41, "v_add_f64": 4.09, "v_cvt_f64_f32": 4.11,
+           "v_cvt_f32_f64": 4.12, "v_pk_mul_f32": 4.09, "v_pk_fma_f32": 4.11, "v_pk_add_f32": 4.1,
+           "v_rndne_f32": 4.06, "v_mov_b64": 4.1}
 
 
 # ordinary ops measured individually by the probe (VGPR operands); others 2.2
@@ -30,6 +34,8 @@ def cost(op):
     base = re.sub(r"_e(32|64)$|_dpp$|_sdwa$", "", op)
     if base in TRANS:
         return 8.1, "trans"
+    if base in COSTF64:
+        return COSTF64[base], "4-cycle"
     if base in COST4:
         return 4.1, "4-cycle"
     return COST2.get(base, 2.2), "2-cycle"
