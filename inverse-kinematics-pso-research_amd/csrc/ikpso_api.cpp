@@ -546,7 +546,7 @@ bool coop_plan(const ChainHost& ch, int mode, int P, int64_t B, bool latency, in
     }
     const int g = (P + T - 1) / T;
     int ng = (geo.cus * geo.blocks_per_cu / g) & ~7;
-    if (g > geo.max_g || ng < 8) return false;
+    if (g > 64 || ng < 8) return false;
     const int64_t want = ((B + 7) / 8) * 8;
     if (want < ng) ng = (int)want;
     *G = g;

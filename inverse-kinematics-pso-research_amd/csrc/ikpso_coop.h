@@ -196,86 +196,16 @@ __device__ __forceinline__ void coop_exchange(SwarmShared<Topo>& sh, CoopShared<
     __syncthreads();
 }
 
-// Per-wave records (kCoopWaveRecords: the long chains' 256-lane chunks, 4 waves
-// each): every wave publishes its OWN record -- the key of its 64 particles' first
-// minimum and that particle's local best -- as soon as its step ends, polls the 4G
-// keys (lane r: record r = member * 4 + wave, i.e. particle-index order, so the
-// first minimum over records is the swarm's first minimum), and on strict
-// improvement takes the winner's vector into sh.g itself.  No workgroup barrier:
-// every wave computes the same winner from the same keys and writes the same
-// vector, and a wave can only write the next gbest after every wave has published
-// (so finished the step that reads the current one).  Records are double-buffered
-// by exchange parity per wave: a wave writes parity p again only after it has
-// seen every record of the exchange in between, which every wave publishes only
-// after it has finished reading parity p.  The chunk argmin's barrier and the
-// closing barrier (wave 0's hand-off, the other waves waiting) go away; what is
-// left of the exchange is each wave's own hop.
-template <class Topo, int BLOCK, class AheadFn>
-__device__ __forceinline__ void coop_exchange_waves(SwarmShared<Topo>& sh, CoopShared<Topo::J>& cs, const float* s_pb,
-                                                    uint32_t local_key, uint32_t& e, int32_t* error,
-                                                    uint32_t spin_limit, bool force, bool do_ahead, AheadFn&& ahead)
-{
-    constexpr int D = Topo::D;
-    constexpr int REC = kCoopRec(D);
-    static_assert(D + 1 <= 64 && BLOCK == 256, "one record per wave of a 4-wave chunk");
-    const int w = wave_id(), lane = lane_id_here();
-    const uint32_t wmin = wave_min_u32(local_key);
-    const int wl = wave_first_lane_eq(local_key, wmin);
-    const int R = 4 * cs.G;  // records of the group (<= 64: checked by the caller)
-    const int rec = cs.member * 4 + w;
-    const granule_t tag = (granule_t)(e + 1) << 32;
-    granule_t* base = cs.slots + (size_t)(e & 1) * R * REC;
-    const float mine_d = lane >= 1 && lane <= D ? s_pb[(lane - 1) * BLOCK + w * 64 + wl] : 0.0f;
-    if (lane <= D) st_granule(base + (size_t)rec * REC + lane, tag | (lane == 0 ? wmin : __float_as_uint(mine_d)));
-    if (do_ahead) ahead();
-    uint32_t n = 0;
-    int timed_out = 0;
-    granule_t kg;
-    for (;;) {
-        kg = lane < R ? ld_granule(base + (size_t)lane * REC) : tag;
-        if (__builtin_amdgcn_ballot_w64((kg >> 32) != (granule_t)(e + 1)) == 0) break;
-        if (spin_limit == 0 || n++ >= spin_limit) {
-            timed_out = 1;
-            break;
-        }
-        __builtin_amdgcn_s_sleep(1);
-    }
-    const uint32_t k = lane < R ? (uint32_t)kg : 0xFFFFFFFFu;
-    const uint32_t gmin = wave_min_u32(k);
-    const int wj = wave_first_lane_eq(k, gmin);
-    if (!timed_out && (force || gmin < cs.gkey)) {  // uniform within the wave; every wave decides alike
-        float gv = mine_d;
-        if (wj != rec) {
-            granule_t vg;
-            for (;;) {
-                vg = lane >= 1 && lane <= D ? ld_granule(base + (size_t)wj * REC + lane) : tag;
-                if (__builtin_amdgcn_ballot_w64((vg >> 32) != (granule_t)(e + 1)) == 0) break;
-                if (n++ >= spin_limit) {
-                    timed_out = 1;
-                    break;
-                }
-            }
-            gv = __uint_as_float((uint32_t)vg);
-        }
-        if (lane >= 1 && lane <= D) sh.g[lane - 1] = gv;
-        if (lane == 0) cs.gkey = gmin;
-    }
-    if (timed_out && lane == 0) {
-        cs.abort = 1;
-        __hip_atomic_store(error, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    ++e;
-}
-
 // Dimensions of the next iteration's update drawn ahead during the exchange,
 // in the throughput build of the FAST tip-backward (long-chain, 2-wave) step:
 // wave 0 draws them between its publish and its poll, the other waves while
 // wave 0 hands off, so the hand-off's wait carries work.  Config 5, 2048 swarms
-// x 4096 x 100: 3 dimensions (node 1) 64.4 -> 63.3 ms; 6 and 9 measured no
-// better than 3 (the extra live values cost the step more than the window saves:
-// profiles/r03b, r03c variant_timings).
+// x 4096 x 100: 3 dimensions (node 1) 64.4 -> 63.3 ms; round 3 measured 6 and 9 no
+// better than 3 (the extra live values spilled); with the velocities updated in
+// their own registers (fma_inplace) the loop has room: 3 / 6 / 9 dimensions
+// 58.36 / 58.22 / 58.08 ms (profiles/r04/variant_timings/var_c5b.txt).
 #ifndef IKPSO_COOP_AHEAD_DIMS
-#define IKPSO_COOP_AHEAD_DIMS 3
+#define IKPSO_COOP_AHEAD_DIMS 9
 #endif
 template <class Topo, int MODE, int TERMS, int BLOCK>
 constexpr int kCoopAhead = (kTipBackward<Topo, MODE, TERMS> && Topo::D > 30) ? IKPSO_COOP_AHEAD_DIMS : 0;
@@ -322,17 +252,6 @@ __global__ void __launch_bounds__(BLOCK, (kCoopMinWaves<Topo::D, BLOCK, TERMS>))
     }
     __syncthreads();
     const PsoCoef coef = pso_coef(cc);
-    // per-wave exchange records (coop_exchange_waves): the long chains' 4-wave chunks, <= 64 records
-    constexpr bool kWaveRecs = IKPSO_COOP_WAVE_RECORDS && D > 30 && BLOCK == 256 && !IKPSO_COOP_TIMING;
-    // (the plan keeps G <= 16 for these builds: CoopGeometry::max_g)
-    uint32_t ew = 0;  // this wave's exchange count (wave records)
-#if IKPSO_COOP_STAGGER > 0
-    // Experiment: start the second half of the grid (the second workgroup of each
-    // CU in dispatch order) IKPSO_COOP_STAGGER x 64 cycles late, so the two swarms
-    // sharing a CU begin out of phase (one's hand-off under the other's step).
-    if (kCoopMinWaves<D, BLOCK, TERMS> > (BLOCK >= 256 ? BLOCK / 256 : 1) && blockIdx.x >= gridDim.x / 2)
-        for (int s = 0; s < IKPSO_COOP_STAGGER; s += 64) __builtin_amdgcn_s_sleep(64);
-#endif
 
     for (;;) {
         compiler_fence();
@@ -365,12 +284,7 @@ __global__ void __launch_bounds__(BLOCK, (kCoopMinWaves<Topo::D, BLOCK, TERMS>))
         float pbf = fitness<Topo, MODE, TERMS>(cc, x, sh.rest, sh.tgt, nullptr, sh.dh, sh.soft);
         // swarm argmin + unconditional first global-best copy (src/kernel.cu:297-304)
         const uint32_t key0 = i < P ? ordered_key(pbf) : 0xFFFFFFFFu;
-        if constexpr (kWaveRecs)
-            coop_exchange_waves<Topo, BLOCK>(sh, cs, s_pb, key0, ew, io.coop_error, io.coop_spin_limit, true,
-                                             io.iterations > 0, ahead);
-        else
-            coop_exchange<Topo, BLOCK>(sh, cs, s_pb, key0, io.coop_error, io.coop_spin_limit, true,
-                                       io.iterations > 0, ahead);
+        coop_exchange<Topo, BLOCK>(sh, cs, s_pb, key0, io.coop_error, io.coop_spin_limit, true, io.iterations > 0, ahead);
 
 #if IKPSO_COOP_TIMING
         unsigned long long t_step = 0, t_bar = 0, t_exch = 0, n_it = 0;
@@ -390,12 +304,8 @@ __global__ void __launch_bounds__(BLOCK, (kCoopMinWaves<Topo::D, BLOCK, TERMS>))
 #if IKPSO_COOP_TIMING
             const unsigned long long t1 = __builtin_amdgcn_s_memtime();
 #endif
-            if constexpr (kWaveRecs)
-                coop_exchange_waves<Topo, BLOCK>(sh, cs, s_pb, key, ew, io.coop_error, io.coop_spin_limit, false,
-                                                 it + 1 < io.iterations, ahead);
-            else
-                coop_exchange<Topo, BLOCK>(sh, cs, s_pb, key, io.coop_error, io.coop_spin_limit, false,
-                                           it + 1 < io.iterations, ahead);
+            coop_exchange<Topo, BLOCK>(sh, cs, s_pb, key, io.coop_error, io.coop_spin_limit, false,
+                                       it + 1 < io.iterations, ahead);
 #if IKPSO_COOP_TIMING
             const unsigned long long t2 = __builtin_amdgcn_s_memtime();
             t_step += t1 - t0;  // wave 0's own step
@@ -418,7 +328,6 @@ __global__ void __launch_bounds__(BLOCK, (kCoopMinWaves<Topo::D, BLOCK, TERMS>))
         }
 #endif
 
-        if constexpr (kWaveRecs) __syncthreads();  // every wave's last exchange is in sh.g / cs.gkey
         compiler_fence();
         const int member = cs.member;
         const int64_t bb = cs.b;

@@ -117,16 +117,6 @@ __host__ __device__ constexpr int kCoopBlocksPerCU()
 #ifndef IKPSO_COOP_TIMING
 #define IKPSO_COOP_TIMING 0  // measurement builds: per-workgroup cycles in the step and in the hand-off
 #endif
-// Per-wave exchange records in the long chains' cooperative kernel (ikpso_coop.h,
-// coop_exchange_waves); 0: one record per chunk behind the chunk argmin's barrier.
-#ifndef IKPSO_COOP_WAVE_RECORDS
-#define IKPSO_COOP_WAVE_RECORDS 0
-#endif
-// Experiment (A/B timing): sleep units of 64 cycles the second workgroup of each CU
-// waits before its first swarm (k_swarm_coop, two workgroups per CU); 0: none.
-#ifndef IKPSO_COOP_STAGGER
-#define IKPSO_COOP_STAGGER 0
-#endif
 // REFERENCE arithmetic on the reference scene with uniform ordered bounds gets its
 // own resident build (no runtime term tests, median clamp); 0: the runtime-term
 // build as before (A/B timing).
@@ -146,10 +136,7 @@ __host__ __device__ constexpr int kCoopBlocksPerCU()
 
 // Published record of one chunk, in 8-byte granules {value, tag}: the key, then
 // the D floats of the chunk winner's local best; padded to a 128-B multiple.
-__host__ __device__ constexpr int kCoopRec(int D) { return ((D + 1 + 15) / 16) * 16; }
-// A chunk's slot: one record, or with per-wave records (the long chains' 4-wave
-// chunks, IKPSO_COOP_WAVE_RECORDS) one per wave.
-__host__ __device__ constexpr int kCoopSlot(int D) { return kCoopRec(D) * (IKPSO_COOP_WAVE_RECORDS && D > 30 ? 4 : 1); }
+__host__ __device__ constexpr int kCoopSlot(int D) { return ((D + 1 + 15) / 16) * 16; }
 // Default bound on a cooperative group wait (polls of ~1 us each): seconds,
 // against ~2 us per exchange when the group is co-resident.
 // IKPSO_COOP_SPIN_LIMIT overrides it (0 forces the give-up path: fallback tests).
@@ -219,7 +206,6 @@ hipError_t launch_coop(const ChainHost& ch, int mode, const SwarmIO& io, hipStre
 // Co-resident workgroups per CU of the cooperative kernel, CU count, threads per workgroup.
 struct CoopGeometry {
     int threads = 0, blocks_per_cu = 0, cus = 0;
-    int max_g = 64;                // chunks per swarm the build's exchange covers (per-wave records: 16)
     bool latency_variant = false;  // a kCoopLatencyThreads build exists for this chain
 };
 bool coop_geometry(const ChainHost& ch, int mode, CoopGeometry* g);

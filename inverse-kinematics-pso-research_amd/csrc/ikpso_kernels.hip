@@ -124,7 +124,6 @@ hipError_t launch_coop(const ChainHost& ch, int mode, const SwarmIO& io, hipStre
     const bool ok = visit_topology(ch, [&](auto topo) {
         using T = decltype(topo);
         if (io.coop_g * kCoopThreads<T::D>() < io.P || io.coop_g > 64) return;  // G chunks must cover the swarm
-        if (IKPSO_COOP_WAVE_RECORDS && T::D > 30 && io.coop_g > 16) return;      // 4G wave records <= 64 lanes
         err = TopoOps<T>::coop(ch, mode, io, stream);
     });
     return ok ? err : hipErrorInvalidValue;
@@ -146,8 +145,6 @@ bool coop_geometry(const ChainHost& ch, int mode, CoopGeometry* g)
             // or the launch could not fit the plan's groups
             g->blocks_per_cu = (ch.num_coll > 0 || ch.poly_trig) ? 1 : kCoopBlocksPerCU<T::D>();
             g->latency_variant = kCoopThreads<T::D>() != kCoopLatencyThreads;
-            // per-wave records: 4 per chunk, one poll lane each (the collider builds too: same kernel)
-            g->max_g = (IKPSO_COOP_WAVE_RECORDS && T::D > 30) ? 16 : 64;
             spec = true;
         }
     });

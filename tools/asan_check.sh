@@ -29,6 +29,7 @@ run)
   timeout -k 10 120 "$OUT/compat_frames" 3 16384
   timeout -k 10 120 "$OUT/batch_c" 64 100
   timeout -k 10 120 "$OUT/compat_frames" 2 300    # ragged particle count (resident / latency paths)
+  timeout -k 10 120 "$OUT/compat_frames" replay 3 2 1024  # the recorded-session replay mode
   echo ASAN_CLEAN
   ;;
 esac
