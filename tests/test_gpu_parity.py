@@ -595,8 +595,8 @@ def test_far_start_pose_inside_narrow_bounds(oracle, device, angle_weight):
     (src/kernel.cu:223-266): with the angle term (weight 3) the unclamped start
     pose keeps the global best and is the answer, returned as it is (the FAST
     kernels hold only in-bounds answers inside the bounds); without it (weight
-    0) the clamped particles win.  Both meet tier A against the oracle (ADVICE
-    r03, low)."""
+    0) the start pose competes on the effector term alone (it still wins some
+    swarms).  Both meet tier A against the oracle."""
     wl = ikpso.workload(3)
     chain = wl.chain.copy()
     chain["min_rotation"][1:] = -1.0
@@ -613,8 +613,6 @@ def test_far_start_pose_inside_narrow_bounds(oracle, device, angle_weight):
     oang, ofit, ores = oracle.solve_batch(chain, tg, sp, P, I, ostate, threads=4, angle_weight=angle_weight)
     if angle_weight > 0:
         assert np.all(oang == sp)  # the start pose wins and comes back unclamped
-    else:
-        assert np.all(np.abs(oang) <= 1.0)
     assert np.max(np.abs(ang - oang)) < 1e-4, np.max(np.abs(ang - oang))
     # with the angle term the reported fitness is the start pose's own initial evaluation, the one
     # evaluation at ~150 rad: the transcendental unit's error there (measured 2.7e-5 relative)
