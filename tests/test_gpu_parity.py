@@ -617,3 +617,25 @@ def test_far_start_pose_inside_narrow_bounds(oracle, device, angle_weight):
     # where the start pose wins, the reported fitness is its own initial evaluation, the one
     # evaluation at ~150 rad: the transcendental unit's error there (measured 2.7e-5 relative)
     assert np.max(np.abs(fit - ofit) / np.maximum(ofit, 1e-6)) < 1e-4
+
+
+@pytest.mark.parametrize("bounds", [(-1.0, 1.0), (2.0, 1.0), (0.0, 0.0)])
+def test_reference_uniform_bounds_builds(oracle, device, bounds):
+    """REFERENCE on the reference tree with uniform clamp bounds: ordered finite
+    bounds take the uniform-bounds build (median clamp, no runtime term tests),
+    inverted ones (lo > hi: the reference's fminf(fmaxf(v, lo), hi) is hi) and
+    degenerate ones the runtime-term build -- every case bit-identical to the
+    oracle (src/matrix_operations.cuh:187-190)."""
+    wl = ikpso.workload(3)
+    chain = wl.chain.copy()
+    chain["min_rotation"][1:] = bounds[0]
+    chain["max_rotation"][1:] = bounds[1]
+    B, P, I = 4, 1024, 20
+    tg = wl.targets(0, B)
+    s = ikpso.BatchSolver(chain, P, pso=wl.pso, arith="reference", kernel="resident")
+    s.seed(B)
+    ang, fit, res = (t.cpu().numpy() for t in s.solve(dev(tg), iterations=I))
+    s.close()
+    ostate = oracle.init_generators(B * P, 0)
+    oang, ofit, ores = oracle.solve_batch(chain, tg, None, P, I, ostate, threads=4)
+    assert np.array_equal(ang, oang) and np.array_equal(fit, ofit)
