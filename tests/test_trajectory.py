@@ -117,3 +117,29 @@ def test_one_step_sample_recomputes(oracle, traj):
     for i in (near, far):
         res = replay(oracle, traj, int(traj["frame"][i]), traj["degrees"][i - 1])
         assert np.array_equal(res, traj["oracle_step"][i]), int(traj["rows"][i])
+
+
+def test_unpinned_rows_are_near_ties(oracle, traj):
+    """The rows the one-step replay does not reproduce to 1e-5 (155 of 661) are
+    another particle of (nearly) the same fitness winning: the reference's
+    logged answer and the replay's score alike under the frame's own fitness
+    (the previous row's pose as the angle term's rest pose, the reset targets) --
+    median |df|/f 4e-5, 91 % within 1e-3, worst 1.1e-2, and the log is better
+    about as often as the replay -- and their residuals agree to 1.6e-3."""
+    ok = ~traj["stale"]
+    rows = np.flatnonzero(ok & (traj["oracle_step_err"] > 1e-5))
+    rel, dres = [], []
+    for i in rows:
+        scene = ikpso.reference_scene(reset=True)
+        if not traj["from_default"][i]:
+            scene.origin.from_coords(traj["degrees"][i - 1].astype(np.float32))
+        chain = scene.origin.to_cuda()
+        logged = traj["degrees"][i].astype(np.float32)
+        f_log, f_rep = oracle.fitness(chain, logged), oracle.fitness(chain, traj["oracle_step"][i])
+        rel.append((float(f_log) - float(f_rep)) / float(f_rep))
+        dres.append(float(oracle.residual(chain, logged)) - float(oracle.residual(chain, traj["oracle_step"][i])))
+    rel, dres = np.array(rel), np.array(dres)
+    assert len(rows) < 0.25 * ok.sum()
+    assert np.median(np.abs(rel)) < 1e-4 and np.mean(np.abs(rel) < 1e-3) > 0.85 and np.abs(rel).max() < 2e-2
+    assert 0.25 < np.mean(rel > 0) < 0.75  # neither side systematically better
+    assert np.abs(dres).max() < 5e-3
