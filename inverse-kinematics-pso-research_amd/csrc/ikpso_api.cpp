@@ -456,7 +456,49 @@ bool build_dh(const std::vector<ikpso_node>& nodes, const ChainHost& eu, const E
 std::mutex g_scratch_mu;
 float* g_scratch = nullptr;
 size_t g_scratch_bytes = 0;
-int32_t* g_err_pinned = nullptr;  // the cooperative error flag's host copy (pinned)
+
+// What the per-frame call keeps between frames (under g_scratch_mu), so that a
+// frame's device work is the solve kernel alone (round 4: the aux upload, the
+// generator snapshot copy, the slot clear and two small D2H copies were 4 extra
+// dependent operations of ~20 us around a 57 us kernel, profiles/r04/frame_*):
+//  * aux: the last uploaded aux block and where it lies; a frame re-uploads only
+//    when its content or place changed (the scene's bounds do not, per frame);
+//  * slots: the cooperative slot region left by the last frame (CoopSlotState);
+//  * pinned: [error flag | answer], written by the kernels themselves (coherent
+//    pinned memory, read after the call's one synchronisation).
+// A cooperative workspace's slot region between launches: [at, at + bytes)
+// holds only zeros or granules tagged below `next`, so a launch there numbers
+// its exchanges from `next` (SwarmIO::coop_tag0) instead of clearing the slots.
+struct CoopSlotState {
+    char* at = nullptr;
+    size_t bytes = 0;
+    uint32_t next = 0;
+    void invalidate() { bytes = 0; }  // something else was written over the region
+    // `exchanges`: an upper bound on the exchanges one group of the launch runs.
+    hipError_t begin(SwarmIO& io, char* ws, size_t zero, uint64_t exchanges, hipStream_t s)
+    {
+        if (at != ws || zero > bytes || exchanges >= 0x7FFFFFFFull || (uint64_t)next + exchanges + 1 >= 0xFFFFFFFFull) {
+            const hipError_t e = hipMemsetAsync(ws, 0, zero, s);
+            if (e != hipSuccess) return e;
+            next = 0;
+        }
+        io.coop_tag0 = next;
+        next = exchanges >= 0x7FFFFFFFull ? 0xFFFFFFFFu : next + (uint32_t)exchanges + 1;  // (cleared next time)
+        at = ws;
+        bytes = zero;  // what lies past it (the snapshot, the fallback's workspace) is not known clean
+        return hipSuccess;
+    }
+};
+
+struct CompatFrameCache {
+    const float* aux_at = nullptr;
+    std::vector<float> aux;
+    CoopSlotState slots;
+    int32_t* pinned = nullptr;      // host address
+    int32_t* pinned_dev = nullptr;  // its device address
+};
+CompatFrameCache g_frame;
+constexpr size_t kFramePinnedWords = 64 + 3 * kMaxJoints;  // the flag, then the answer at word 64
 
 ikpso_status scratch(size_t bytes, float** out)
 {
@@ -464,11 +506,24 @@ ikpso_status scratch(size_t bytes, float** out)
         if (g_scratch) (void)hipFree(g_scratch);
         g_scratch = nullptr;
         g_scratch_bytes = 0;
+        g_frame.aux_at = nullptr;  // nothing of the old block is known to survive
+        g_frame.slots.invalidate();
         IKPSO_HIP(hipMalloc(&g_scratch, bytes));
         g_scratch_bytes = bytes;
     }
     *out = g_scratch;
     return IKPSO_OK;
+}
+
+// True when `p` is device memory (a kernel writes it directly; anything else --
+// pageable, pinned or managed host memory -- gets the answer through the pinned block).
+bool is_device_memory(const void* p)
+{
+    const hipError_t prior = hipPeekAtLastError();
+    hipPointerAttribute_t a{};
+    const hipError_t e = hipPointerGetAttributes(&a, p);
+    if (e != hipSuccess && prior == hipSuccess) (void)hipGetLastError();  // see fetch_any
+    return e == hipSuccess && a.type == hipMemoryTypeDevice;
 }
 
 // Carve 256-byte aligned arrays out of one allocation.
@@ -579,9 +634,13 @@ uint32_t coop_spin_limit()
 }
 
 // Point the coop fields of `io` into workspace `ws` (coop_workspace_bytes) and
-// clear the counters and the error flag.
-hipError_t carve_coop(SwarmIO& io, void* ws, int G, int NG, int block, int D, hipStream_t s, bool linear = false)
+// clear the error flag and the slots (unless !clear: the caller numbers the
+// exchanges past the tags the slots hold, io.coop_tag0).  *zero_bytes: the
+// extent of the flag + slots from `ws`.
+hipError_t carve_coop(SwarmIO& io, void* ws, int G, int NG, int block, int D, hipStream_t s, bool linear = false,
+                      bool clear = true, size_t* zero_bytes = nullptr)
 {
+    io.coop_tag0 = 0;
     io.coop_spin_limit = coop_spin_limit();
     io.coop_linear = linear ? 1 : 0;
     Carver cv{static_cast<char*>(ws)};
@@ -594,11 +653,12 @@ hipError_t carve_coop(SwarmIO& io, void* ws, int G, int NG, int block, int D, hi
     // the error flag and every granule's tag start at 0 (tags are exchange numbers + 1)
     const size_t zero = reinterpret_cast<char*>(io.coop_slots + (size_t)NG * 2 * G * kCoopSlot(D)) -
                         static_cast<char*>(ws);
+    if (zero_bytes) *zero_bytes = zero;
     if (IKPSO_COOP_TIMING) {
         const hipError_t e = hipMemsetAsync(io.coop_timing, 0, (size_t)NG * G * 64, s);
         if (e != hipSuccess) return e;
     }
-    return hipMemsetAsync(ws, 0, zero, s);
+    return clear ? hipMemsetAsync(ws, 0, zero, s) : hipSuccess;
 }
 
 // Resolve the kernel family for a chain and swarm size; -1 if impossible.
@@ -648,10 +708,13 @@ struct ikpso_solver {
         int32_t iterations = 0;
         float *out_angles = nullptr, *out_fitness = nullptr, *out_residual = nullptr;
         hipStream_t stream = nullptr;
-        const int32_t* error = nullptr;  // device flag in ws
     } pending;
     int64_t fallbacks = 0;
-    int32_t* err_host = nullptr;  // pinned host copy of a cooperative solve's error flag (ikpso_solver_sync)
+    // a cooperative solve's error flag, in coherent pinned memory the kernel writes
+    // (read by ikpso_solver_sync after its synchronisation), and its device address
+    int32_t* err_host = nullptr;
+    int32_t* err_dev = nullptr;
+    CoopSlotState slots;  // the cooperative slots in `ws` between solves
 #if IKPSO_COOP_TIMING
     unsigned long long* pending_timing = nullptr;
     int pending_timing_n = 0;
@@ -680,6 +743,7 @@ ikpso_status solve_streaming(ikpso_solver* s, void** ws, size_t* ws_bytes, const
 {
     const ChainHost& ch = s->solve_chain();
     const int D = ch.kernel_dims();
+    s->slots.invalidate();  // the streaming workspace overwrites the cooperative slots
     ikpso_status st = grow(ws, ws_bytes, stream_workspace_bytes(num_swarms, s->P, D, true));
     if (st != IKPSO_OK) return st;
     StreamIO io{};
@@ -782,28 +846,50 @@ ikpso_status ikpso_calculate_pso(float* particles, const float* positions, float
         return IKPSO_ERR_UNSUPPORTED;
 
     std::lock_guard<std::mutex> lk(g_scratch_mu);
-    // device scratch: [result D | aux (64-float aligned) | workspace]; aux is
-    // uploaded here and the call synchronises before returning, so `ch.aux`
-    // outlives every use.  The cooperative path also keeps a snapshot of the
-    // generator states and room for the streaming fallback.
+    // device scratch: [aux (at float ceil64(D)) | workspace]; aux is uploaded here (when
+    // it changed) and the call synchronises before returning, so `ch.aux` outlives
+    // every use.  The cooperative path also keeps a snapshot of the generator
+    // states (written by the kernel as it loads them) and room for the streaming
+    // fallback.  The answer goes to `result` directly when that is device memory,
+    // else to the pinned block, copied out after the synchronisation.
     const size_t aux_at = ((size_t)D + 63) & ~size_t(63);
     const size_t head = sizeof(float) * (aux_at + ch.aux.size());
     const size_t sws = stream_workspace_bytes(1, size, D, false);
     const size_t snap = ((sizeof(ikpso_rng_state) * (size_t)size + 255) & ~size_t(255));
+    const size_t cws = family_run == IKPSO_KERNEL_COOP ? ((coop_workspace_bytes(cng, cg, D, cblk) + 255) & ~size_t(255)) : 0;
     const size_t ws = family_run == IKPSO_KERNEL_STREAMING ? sws
-                      : family_run == IKPSO_KERNEL_COOP
-                          ? ((coop_workspace_bytes(cng, cg, D, cblk) + 255) & ~size_t(255)) + snap + sws
-                          : 0;
+                      : family_run == IKPSO_KERNEL_COOP ? cws + snap + sws
+                                                          : 0;
     float* dres = nullptr;
     st = scratch(((head + 255) & ~size_t(255)) + ws, &dres);
     if (st != IKPSO_OK) return st;
+    if (!g_frame.pinned) {
+        void* h = nullptr;
+        IKPSO_HIP(hipHostMalloc(&h, sizeof(int32_t) * kFramePinnedWords, hipHostMallocCoherent | hipHostMallocMapped));
+        void* dv = nullptr;
+        const hipError_t e = hipHostGetDevicePointer(&dv, h, 0);
+        if (e != hipSuccess) {
+            (void)hipHostFree(h);
+            IKPSO_HIP(e);
+        }
+        g_frame.pinned = static_cast<int32_t*>(h);
+        g_frame.pinned_dev = static_cast<int32_t*>(dv);
+    }
+    const bool direct = is_device_memory(result);
+    float* const out = direct ? result : reinterpret_cast<float*>(g_frame.pinned_dev + 64);
     const hipStream_t s = (hipStream_t)stream;
-    IKPSO_HIP(hipMemcpyAsync(dres + aux_at, ch.aux.data(), sizeof(float) * ch.aux.size(), hipMemcpyHostToDevice, s));
+    if (g_frame.aux_at != dres + aux_at || g_frame.aux != ch.aux) {
+        IKPSO_HIP(hipMemcpyAsync(dres + aux_at, ch.aux.data(), sizeof(float) * ch.aux.size(), hipMemcpyHostToDevice, s));
+        g_frame.aux_at = dres + aux_at;
+        g_frame.aux = ch.aux;
+    }
     ch.aux_dev = dres + aux_at;
+    char* const wsb = reinterpret_cast<char*>(dres) + ((head + 255) & ~size_t(255));
+    if (family_run != IKPSO_KERNEL_COOP) g_frame.slots.invalidate();  // the streaming workspace overwrites the slots
     if (family_run == IKPSO_KERNEL_RESIDENT) {
         SwarmIO io{};
         io.rng = randoms;
-        io.out_angles = dres;
+        io.out_angles = out;
         io.dump_particles = particles;
         io.dump_bests = bests;
         io.P = size;
@@ -813,27 +899,22 @@ ikpso_status ikpso_calculate_pso(float* particles, const float* positions, float
     } else if (family_run == IKPSO_KERNEL_COOP) {
         SwarmIO io{};
         io.rng = randoms;
-        io.out_angles = dres;
+        io.out_angles = out;
         io.dump_particles = particles;
         io.dump_bests = bests;
         io.P = size;
         io.iterations = pso.iterations;
         io.num_swarms = 1;
-        char* wsb = reinterpret_cast<char*>(dres) + ((head + 255) & ~size_t(255));
-        ikpso_rng_state* rsnap =
-            reinterpret_cast<ikpso_rng_state*>(wsb + ((coop_workspace_bytes(cng, cg, D, cblk) + 255) & ~size_t(255)));
-        IKPSO_HIP(hipMemcpyAsync(rsnap, randoms, sizeof(ikpso_rng_state) * (size_t)size, hipMemcpyDeviceToDevice, s));
-        IKPSO_HIP(carve_coop(io, wsb, cg, cng, cblk, D, s, clin));
+        ikpso_rng_state* const rsnap = reinterpret_cast<ikpso_rng_state*>(wsb + cws);
+        io.rng_snap = rsnap;  // one swarm, started by its group: the snapshot is complete
+        size_t zero = 0;
+        IKPSO_HIP(carve_coop(io, wsb, cg, cng, cblk, D, s, clin, false, &zero));
+        IKPSO_HIP(g_frame.slots.begin(io, wsb, zero, (uint64_t)pso.iterations + 1, s));  // one swarm: I + 1 exchanges
+        io.coop_error = g_frame.pinned_dev;
+        __atomic_store_n(g_frame.pinned, 0, __ATOMIC_RELEASE);
         IKPSO_HIP(launch_coop(ch, mode, io, s));
-        // the error flag (into pinned memory: a truly asynchronous copy) and the
-        // answer come back behind ONE synchronisation; a fallback rewrites the answer
-        if (!g_err_pinned) IKPSO_HIP(hipHostMalloc(reinterpret_cast<void**>(&g_err_pinned), sizeof(int32_t)));
-        *g_err_pinned = 0;
-        IKPSO_HIP(hipMemcpyAsync(g_err_pinned, io.coop_error, sizeof(int32_t), hipMemcpyDeviceToHost, s));
-        IKPSO_HIP(hipMemcpyAsync(result, dres, sizeof(float) * D, hipMemcpyDefault, s));
         IKPSO_HIP(hipStreamSynchronize(s));
-        if (!*g_err_pinned) return IKPSO_OK;
-        {
+        if (__atomic_load_n(g_frame.pinned, __ATOMIC_ACQUIRE) != 0) {
             // The group could not assemble (other work held CUs): restore the
             // generator states and solve on the streaming kernels, which need
             // no co-residency -- the caller never sees the contention.
@@ -844,21 +925,22 @@ ikpso_status ikpso_calculate_pso(float* particles, const float* positions, float
             sio.state = particles;
             sio.pbf = bests;
             sio.rng_aos = randoms;
-            sio.out_angles = dres;
+            sio.out_angles = out;
             IKPSO_HIP(launch_stream(ch, mode, sio, pso.iterations, s));
             g_coop_fallbacks.fetch_add(1);
+            IKPSO_HIP(hipStreamSynchronize(s));
         }
     } else {
         StreamIO io{};
-        carve_stream(io, reinterpret_cast<char*>(dres) + ((head + 255) & ~size_t(255)), 1, size, D, false);
+        carve_stream(io, wsb, 1, size, D, false);
         io.state = particles;  // the reference's own [3][D][P] layout is the streaming state
         io.pbf = bests;
         io.rng_aos = randoms;
-        io.out_angles = dres;
+        io.out_angles = out;
         IKPSO_HIP(launch_stream(ch, mode, io, pso.iterations, s));
     }
-    IKPSO_HIP(hipMemcpyAsync(result, dres, sizeof(float) * D, hipMemcpyDefault, s));
-    IKPSO_HIP(hipStreamSynchronize(s));
+    if (family_run != IKPSO_KERNEL_COOP) IKPSO_HIP(hipStreamSynchronize(s));
+    if (!direct) memcpy(result, g_frame.pinned + 64, sizeof(float) * D);
     return IKPSO_OK;
 }
 
@@ -1032,10 +1114,26 @@ ikpso_status ikpso_solve_batch(ikpso_solver* s, const float* targets, const floa
         bool linear = false;
         if (!coop_plan(ch, s->mode, s->P, num_swarms, s->requested == IKPSO_KERNEL_AUTO, &G, &NG, &T, &linear))
             return IKPSO_ERR_UNSUPPORTED;
+        const size_t had = s->ws_bytes;
         ikpso_status st = grow(&s->ws, &s->ws_bytes, coop_workspace_bytes(NG, G, D, T));
         if (st != IKPSO_OK) return st;
+        if (s->ws_bytes != had) s->slots.invalidate();  // a new allocation: contents unknown
+        if (!s->err_host) {
+            void* h = nullptr;
+            IKPSO_HIP(hipHostMalloc(&h, sizeof(int32_t), hipHostMallocCoherent | hipHostMallocMapped));
+            void* dv = nullptr;
+            const hipError_t e = hipHostGetDevicePointer(&dv, h, 0);
+            if (e != hipSuccess) {
+                (void)hipHostFree(h);
+                IKPSO_HIP(e);
+            }
+            s->err_host = static_cast<int32_t*>(h);
+            s->err_dev = static_cast<int32_t*>(dv);
+        }
         // snapshot of the generator states the launch starts from (48 B per
-        // particle, one D2D copy): the fallback re-runs the batch from it
+        // particle): the fallback re-runs the batch from it.  One swarm: the kernel
+        // writes it as its chunks load the states; more: one D2D copy before the
+        // launch (a group that gives up never loads its later swarms)
         if (num_swarms > s->snap_capacity) {
             if (s->rng_snap) IKPSO_HIP(hipFree(s->rng_snap));
             s->rng_snap = nullptr;
@@ -1043,9 +1141,11 @@ ikpso_status ikpso_solve_batch(ikpso_solver* s, const float* targets, const floa
             IKPSO_HIP(hipMalloc(&s->rng_snap, sizeof(ikpso_rng_state) * (size_t)s->capacity * s->P));
             s->snap_capacity = s->capacity;
         }
-        IKPSO_HIP(hipMemcpyAsync(s->rng_snap, s->rng, sizeof(ikpso_rng_state) * (size_t)num_swarms * s->P,
-                                 hipMemcpyDeviceToDevice, hs));
+        if (num_swarms > 1)
+            IKPSO_HIP(hipMemcpyAsync(s->rng_snap, s->rng, sizeof(ikpso_rng_state) * (size_t)num_swarms * s->P,
+                                     hipMemcpyDeviceToDevice, hs));
         SwarmIO io{};
+        io.rng_snap = num_swarms == 1 ? s->rng_snap : nullptr;
         io.targets = targets;
         io.start_pose = start_pose;
         io.rng = s->rng;
@@ -1055,7 +1155,12 @@ ikpso_status ikpso_solve_batch(ikpso_solver* s, const float* targets, const floa
         io.P = s->P;
         io.iterations = iterations;
         io.num_swarms = num_swarms;
-        IKPSO_HIP(carve_coop(io, s->ws, G, NG, T, D, hs, linear));
+        size_t zero = 0;
+        IKPSO_HIP(carve_coop(io, s->ws, G, NG, T, D, hs, linear, false, &zero));
+        // a group runs at most every swarm: B (I + 1) exchanges bound its numbering
+        IKPSO_HIP(s->slots.begin(io, static_cast<char*>(s->ws), zero, (uint64_t)num_swarms * ((uint64_t)iterations + 1), hs));
+        io.coop_error = s->err_dev;
+        *s->err_host = 0;  // the previous solve has settled: nothing writes it now
         // the reported name follows the variant that runs (long chains' throughput chunks are
         // kCoopLatencyThreads wide too: only a block other than the throughput one is the latency plan)
         CoopGeometry geo;
@@ -1070,7 +1175,6 @@ ikpso_status ikpso_solve_batch(ikpso_solver* s, const float* targets, const floa
         s->pending.out_fitness = out_fitness;
         s->pending.out_residual = out_residual;
         s->pending.stream = hs;
-        s->pending.error = io.coop_error;
 #if IKPSO_COOP_TIMING
         s->pending_timing = io.coop_timing;
         s->pending_timing_n = NG * G;
@@ -1090,12 +1194,9 @@ ikpso_status ikpso_solver_sync(ikpso_solver* s)
     // up, the fallback has run: a failure on the way (an allocation, a copy)
     // returns its error and leaves the solve pending, so the next sync, solve or
     // generator_states call settles it instead of reporting OK over NaN answers.
-    // into pinned memory: a truly asynchronous copy, one synchronisation
-    if (!s->err_host) IKPSO_HIP(hipHostMalloc(reinterpret_cast<void**>(&s->err_host), sizeof(int32_t)));
-    *s->err_host = 0;
-    IKPSO_HIP(hipMemcpyAsync(s->err_host, p.error, sizeof(int32_t), hipMemcpyDeviceToHost, p.stream));
+    // the kernel writes the flag into coherent pinned memory: one synchronisation
     IKPSO_HIP(hipStreamSynchronize(p.stream));
-    const int32_t err = *s->err_host;
+    const int32_t err = __atomic_load_n(s->err_host, __ATOMIC_ACQUIRE);
 #if IKPSO_COOP_TIMING
     if (s->pending_timing) {  // measurement build: mean cycles per iteration over the workgroups
         std::vector<unsigned long long> t((size_t)s->pending_timing_n * 8);

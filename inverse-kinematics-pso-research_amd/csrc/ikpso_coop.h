@@ -28,7 +28,10 @@
 // fence.  Records are double-buffered by exchange parity: a chunk rewrites
 // parity p only after it has seen every chunk's record of the previous
 // exchange, by which time every chunk has finished reading parity p.  The
-// slots are zeroed before every launch (tag 0 never matches).  Workgroup b sits
+// slots hold zeros or the tags of earlier launches: a launch numbers its
+// exchanges past them (io.coop_tag0; the host zeroes the slots when the
+// numbering would wrap or the region was used for something else), so neither
+// tag 0 nor a stale tag ever matches.  Workgroup b sits
 // on XCD b % 8; the G chunks of a group share an XCD (speed only, never
 // correctness) -- except a latency group wider than an XCD (the visualiser's
 // N = 16384: 64 chunks), which takes linear membership and hands off across
@@ -187,7 +190,8 @@ __device__ __forceinline__ void coop_exchange(SwarmShared<Topo>& sh, CoopShared<
             cs.e = e + 1;
             if (timed_out) {
                 cs.abort = 1;
-                __hip_atomic_store(error, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                // system scope: the flag may live in pinned host memory (the per-frame call)
+                __hip_atomic_store(error, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             }
         }
     } else if (do_ahead) {
@@ -242,7 +246,7 @@ __global__ void __launch_bounds__(BLOCK, (kCoopMinWaves<Topo::D, BLOCK, TERMS>))
         coop_membership(io, &group, &member);
         cs.G = G;
         cs.member = member;
-        cs.e = 0;
+        cs.e = io.coop_tag0;
         cs.abort = 0;
         cs.b = group;
 #if IKPSO_COOP_TIMING
@@ -267,7 +271,10 @@ __global__ void __launch_bounds__(BLOCK, (kCoopMinWaves<Topo::D, BLOCK, TERMS>))
         using Rng = XorwowT<((kOwnCU && BLOCK == kCoopLatencyThreads) || D > 30) &&
                             std::is_same_v<RngFor<TERMS>, XorwowT<true>>>;
         Rng rng{0, 0, 0, 0, 0, 0};
-        if (i < P) load_rng(rng, io.rng + b * P + i);
+        if (i < P) {
+            if (io.rng_snap) io.rng_snap[b * P + i] = io.rng[b * P + i];  // the whole 48-byte state
+            load_rng(rng, io.rng + b * P + i);
+        }
         if (tid == 0) cs.gkey = 0xFFFFFFFFu;
         __syncthreads();
 
@@ -555,7 +562,7 @@ __global__ void __launch_bounds__(2 * kCoopLatencyThreads) k_swarm_coop_split(co
         coop_membership(io, &group, &member);
         cs.G = G;
         cs.member = member;
-        cs.e = 0;
+        cs.e = io.coop_tag0;
         cs.abort = 0;
         cs.b = group;
 #if IKPSO_COOP_TIMING
@@ -576,7 +583,10 @@ __global__ void __launch_bounds__(2 * kCoopLatencyThreads) k_swarm_coop_split(co
         Rng rng{0, 0, 0, 0, 0, 0};
         const int I = io.iterations;
         if (gen) {
-            if (i < P) load_rng(rng, io.rng + b * P + i);
+            if (i < P) {
+                if (io.rng_snap) io.rng_snap[b * P + i] = io.rng[b * P + i];
+                load_rng(rng, io.rng + b * P + i);
+            }
             gen_quads<D, 0, NQI, BC, -1>(rng, lds.draws[0] + lc, coef);  // block 0: initParticlesKernel's draws
         }
         if (tid == 0) cs.gkey = 0xFFFFFFFFu;

@@ -68,9 +68,10 @@ struct SwarmIO {
     int32_t iterations;
     int64_t num_swarms;
     // cooperative kernel only (ikpso_coop.h): G workgroups per swarm, NG groups
-    unsigned long long* coop_slots;  // [NG][2][G][kCoopSlot(D)] granules {value, tag}: the chunk minima (zeroed
-                                     // before the launch)
-    int32_t* coop_error;      // set to 1 if a group wait timed out
+    unsigned long long* coop_slots;  // [NG][2][G][kCoopSlot(D)] granules {value, tag}: the chunk minima (zero, or
+                                     // tags below coop_tag0 + 1, before the launch)
+    int32_t* coop_error;      // set to 1 if a group wait timed out (device or pinned host memory;
+                              // the kernels only write it)
     int32_t coop_g;
     int32_t coop_ng;
     int32_t coop_block;       // workgroup size (kCoopThreads<J>() or kCoopLatencyThreads)
@@ -78,6 +79,16 @@ struct SwarmIO {
     unsigned long long* coop_timing;  // IKPSO_COOP_TIMING builds: [NG*G][4] cycle counts (else null)
     int32_t coop_linear;      // membership: 0 = XCD-aware (a group on one XCD, NG a multiple of 8),
                               // 1 = linear (group = workgroup / G: a latency group wider than an XCD)
+    // The first exchange number of this launch: granule tags run tag0 + 1 ..
+    // tag0 + exchanges, so granules a previous launch left (smaller tags) never
+    // match and the slots need no clearing between launches (the per-frame call;
+    // 0 with freshly zeroed slots otherwise).
+    uint32_t coop_tag0;
+    // Optional [B][P] copy of the generator states, written as each chunk loads
+    // them (what a streaming re-run restarts from), or null.  Complete only when
+    // every swarm is started in the launch's first round (the hosts pass it for
+    // one swarm: a group that gives up never loads its later swarms).
+    ikpso_rng_state* rng_snap;
 };
 
 // Streaming (state-in-HBM) kernels: one launch per PSO iteration over every

@@ -117,9 +117,14 @@ def test_auto_reports_latency_variant(device):
 # assembling.  The solve must still complete -- restored generator states,
 # re-run on the streaming kernels -- with the results a streaming solve gives.
 
-def test_coop_forced_timeout_falls_back_batch(device, monkeypatch):
+@pytest.mark.parametrize("B", [1, 6])
+def test_coop_forced_timeout_falls_back_batch(device, monkeypatch, B):
+    """B = 6: the snapshot is a copy before the launch; B = 1: the kernel writes
+    it as its chunks load the states.  Then two more solves on the same solvers
+    (the slots re-cleared after the fallback's streaming pass, then numbered
+    past the last solve's tags) still equal the streaming solver's."""
     wl = ikpso.workload(3)
-    B, P, I = 6, 16384, 5
+    P, I = 16384, 5
     tg = dev(wl.targets(0, B))
     out = {}
     for name, kern, spin in (("coop", "coop", "0"), ("streaming", "streaming", None)):
@@ -137,7 +142,13 @@ def test_coop_forced_timeout_falls_back_batch(device, monkeypatch):
             before = s.fallbacks
             s.sync()  # ... and sync re-runs the batch from the snapshot
             assert s.fallbacks == before + 1
-        out[name] = [t.cpu().numpy() for t in (a0, f0, r0)]
+            monkeypatch.delenv("IKPSO_COOP_SPIN_LIMIT", raising=False)
+        res = [t.cpu().numpy() for t in (a0, f0, r0)]
+        for _ in range(2):
+            res += [t.cpu().numpy() for t in s.solve(tg, iterations=I)]
+        if kern == "coop":
+            assert s.fallbacks == before + 1
+        out[name] = res
         s.close()
     for x, y in zip(out["coop"], out["streaming"]):
         assert np.array_equal(x, y)
@@ -166,6 +177,57 @@ def test_coop_forced_timeout_falls_back_compat(oracle, device, monkeypatch):
     assert np.array_equal(bests.cpu().numpy(), obests)
     assert np.array_equal(parts.cpu().numpy(), oparts)
     assert np.array_equal(res, ores)
+
+
+def test_compat_frames_across_families_and_fallback(oracle, device, monkeypatch):
+    """The per-frame call keeps its aux block, its cooperative slots (exchanges
+    numbered past the last frame's tags instead of cleared) and its generator
+    snapshot (written by the kernel) between frames.  A sequence that changes
+    what lies in the scratch under it -- streaming frames over the slots, a
+    forced fallback, another swarm size, new distance-term positions, the answer
+    into device memory -- stays the oracle's bit for bit, frame after frame."""
+    monkeypatch.setenv("IKPSO_ARITH", "reference")
+    monkeypatch.delenv("IKPSO_COOP_SPIN_LIMIT", raising=False)
+    monkeypatch.delenv("IKPSO_KERNEL", raising=False)
+    lib = ikpso.load()
+    scene = ikpso.reference_scene(reset=True)
+    D, I = 21, 3
+    streams = {}
+    for n in (16384, 512):
+        r = ikpso.rng_tensor(n)
+        assert ikpso.init_generators(r, n) == 0
+        streams[n] = (r, oracle.init_generators(n, 0), ikpso.particles_tensor(n, D),
+                      torch.zeros(n, dtype=torch.float32, device="cuda"))
+    pos0 = scene.origin.fill_positions()
+    steps = [dict(), dict(kernel="streaming"), dict(), dict(spin="0"), dict(), dict(device_result=True),
+             dict(n=512), dict(), dict(positions=pos0), dict(positions=pos0 + 0.25), dict(), dict()]
+    pose = None
+    for k, stp in enumerate(steps):
+        n = stp.get("n", 16384)
+        r, ost, parts, bests = streams[n]
+        for var, val in (("IKPSO_KERNEL", stp.get("kernel")), ("IKPSO_COOP_SPIN_LIMIT", stp.get("spin"))):
+            if val is None:
+                monkeypatch.delenv(var, raising=False)
+            else:
+                monkeypatch.setenv(var, val)
+        if pose is not None:
+            scene.origin.from_coords(pose)
+        chain = scene.origin.to_cuda()
+        pos = stp.get("positions")
+        fit = ikpso.FitnessConfig(3.0, 1.0 if pos is not None else 0.0, 0.1)
+        res = torch.zeros(D, dtype=torch.float32, device="cuda") if stp.get("device_result") else \
+            np.zeros(D, dtype=np.float32)
+        before = lib.ikpso_coop_fallbacks()
+        assert ikpso.calculate_pso(parts, pos, bests, r, n, chain, ikpso.PSOConfig(0.5, 0.5, 1.25, I), fit, res) == 0
+        assert lib.ikpso_coop_fallbacks() == before + (1 if stp.get("spin") == "0" else 0), k
+        ores, oparts, obests = oracle.calculate_pso(chain, n, ost, iterations=I, distance_weight=fit.distance_weight,
+                                                    positions=pos)
+        got = res.cpu().numpy() if isinstance(res, torch.Tensor) else res
+        assert np.array_equal(got, ores), (k, stp)
+        assert np.array_equal(bests.cpu().numpy(), obests), (k, stp)
+        assert np.array_equal(r.cpu().numpy()[:, :6], ost.view(np.int32).reshape(n, 12)[:, :6]), (k, stp)
+        if n == 16384:
+            pose = got.copy()
 
 
 def test_solve_rejects_wrong_dtype_and_device(device):
