@@ -15,6 +15,7 @@
 #   profile:<n>  kernel trace + PMC passes (tools/gpu_profile.sh) of workload n in
 #                {c3, c5, dh7, c3ref}: the counters bench.py's roofline reads
 #   frame        the visualiser frame latency (tools/frame_bench.py)
+#   frametrace   rocprofv3 kernel trace of the same (what device work one frame issues)
 #   var:<out>    interleaved variant timing (tools/gpu_var.sh; VAR_ARGS = "CONFIG SWARMS ITERS LIB...")
 #   asan         host-code ASan/UBSan run (tools/asan_check.sh)
 #
@@ -56,6 +57,9 @@ for s in "$@"; do
     profile:c5) PROF_NAME=c5 PROF_ARGS="--config 5 --swarms-per-gpu 2048 --iterations 100 --steps 1 --warmup 1 \
                 --cpu-seconds 0" bash tools/gpu_profile.sh || exit 6 ;;
     frame) step frame 300 python tools/frame_bench.py || exit 7 ;;
+    frametrace)
+      step frametrace 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_frame -o run --output-format csv -- \
+        python3 tools/frame_bench.py || exit 7 ;;
     var:*) bash tools/gpu_var.sh "${s#var:}" $VAR_ARGS || exit 8 ;;
     asan) step asan 600 bash tools/asan_check.sh run || exit 9 ;;
     *) echo "unknown stage $s"; exit 64 ;;
