@@ -200,8 +200,10 @@ int main(int argc, char** argv)
             const auto t0 = std::chrono::steady_clock::now();
             const hipError_t st = calculatePSO(particles, positions, bests, randoms, N, chain, pso, fit, result,
                                                colliders, 0);
-            solve_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-            ++solves;
+            if (c > 0 || f > 1) {  // the first call (code-object load, first allocations) is warm-up
+                solve_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+                ++solves;
+            }
             if (st != hipSuccess) {  // the frame loop breaks on a failed solve (src/Main.cpp:226)
                 fprintf(stderr, "calculatePSO failed: %s\n", hipGetErrorString(st));
                 return 2;
