@@ -45,12 +45,20 @@ constexpr int kPrioLevels2Wave = IKPSO_PRIO_LEVELS_2WAVE, kPrioLevels4Wave = 2;
 // one runs its tail alone, with nothing to hide its dependency latency.
 // With 4 waves per SIMD, 2 levels (4 keep them in lockstep, contending for the
 // same unit at the same time).
-template <int J, int L>
+// INV: the other way round -- a wave later in its step ranks higher.  The
+// long-chain cooperative kernel (config 5) holds two workgroups of DIFFERENT
+// swarms per CU, one wave of each per SIMD; ranked by progress they lock in
+// phase and reach their exchanges together, leaving the SIMD idle while both
+// wait.  Ranked the other way the one ahead finishes its step first and hands
+// off while the other computes: 58.1 -> 57.1 ms on 2048 swarms x 4096 x 100,
+// 232.6 -> 228.5 ms on 8192 (profiles/r04/variant_timings/var_c5inv*.txt; 2
+// levels inverted: 60.7 ms, 4: 57.1 ms).
+template <int J, int L, bool INV = false>
 __device__ __forceinline__ void progress_prio(int k)
 {
     static_assert(L == 0 || (L >= 2 && L <= 4), "priority levels: none or 2..4");
     if constexpr (L > 0) {
-        switch ((L - 1) - (L * (k - 1)) / J) {
+        switch (INV ? (L * (k - 1)) / J : (L - 1) - (L * (k - 1)) / J) {
         case 3: __builtin_amdgcn_s_setprio(3); break;
         case 2: __builtin_amdgcn_s_setprio(2); break;
         case 1: __builtin_amdgcn_s_setprio(1); break;
@@ -148,7 +156,7 @@ __device__ __forceinline__ void swarm_step_tip(const ChainConsts<Topo::J>& cc, S
     }
 #pragma unroll
     for (int k = 1; k <= J; ++k) {
-        progress_prio<2 * J, PL>(k);
+        progress_prio<2 * J, PL, (KA > 0)>(k);  // KA > 0: the cooperative build (two swarms per CU)
         float cpb[A], cg[A], crest[A];
 #pragma unroll
         for (int ax = 0; ax < A; ++ax) {
@@ -183,7 +191,7 @@ __device__ __forceinline__ void swarm_step_tip(const ChainConsts<Topo::J>& cc, S
     NodeTrig<A> cur = node_trig<Acc::HW, A>(x + A * (J - 1));
 #pragma unroll
     for (int k = J; k >= 1; --k) {
-        progress_prio<2 * J, PL>(2 * J + 1 - k);
+        progress_prio<2 * J, PL, (KA > 0)>(2 * J + 1 - k);
         NodeTrig<A> nxt = cur;
         if (k > 1) nxt = node_trig<Acc::HW, A>(x + A * (k - 2));
         acc.back(cc, k, cur);
