@@ -246,7 +246,10 @@ __device__ __forceinline__ void swarm_step(const ChainConsts<Topo::J>& cc, Swarm
     for (int c = 0; c < 3; ++c) ntgt[c] = Topo::effector(1) ? sh.tgt[c] : 0.0f;
 #pragma unroll
     for (int k = 1; k <= J; ++k) {
-        progress_prio<J, (D > kTrigAheadMaxD ? kPrioLevels2Wave : 0)>(k);  // the 2-wave kernels
+        // the 2-wave kernels, and (D <= 30: only REFERENCE arithmetic takes this path) the
+        // 4-wave ones: 2 levels, 16.98 -> 15.85 ms on the REFERENCE config-3 shape (2048 x
+        // 1024 x 200, profiles/r04/variant_timings/var_refprio.txt; 3 levels 15.89)
+        progress_prio<J, (D > kTrigAheadMaxD ? kPrioLevels2Wave : kPrioLevels4Wave)>(k);
         float cpb[A], cg[A], crest[A], ctgt[3];
 #pragma unroll
         for (int ax = 0; ax < A; ++ax) {
