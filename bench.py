@@ -53,6 +53,9 @@ def parse():
     ap.add_argument("--particles", type=int, default=None)
     ap.add_argument("--iterations", type=int, default=None)
     ap.add_argument("--arith", choices=["fast", "reference"], default="fast")
+    ap.add_argument("--colliders", choices=["none", "init03", "init4", "far4"], default="none",
+                    help="config 3 with the reference's initColliders boxes (src/Main.cpp:537-559): 0 and 3, all "
+                         "four, or all four moved 1000 units away (the collider kernel with nothing near)")
     ap.add_argument("--kernel", choices=["auto", "resident", "coop", "streaming"], default="auto",
                     help="kernel family (auto: resident if the swarm fits one workgroup, else cooperative)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU baseline sample (0 = skip)")
@@ -61,11 +64,15 @@ def parse():
     ap.add_argument("--reference-steps", type=int, default=3,
                     help="after the FAST legs, time this many steps of the same workload in REFERENCE arithmetic "
                          "(the bit-exact path; rank 0, configs 3/4; 0 = skip)")
-    ap.add_argument("--extra-legs", default="4,5,dh7",
+    ap.add_argument("--extra-legs", default="4,5,dh7,collide",
                     help="with the default config 3: also time these BASELINE lines in the same run and print them "
-                         "under 'legs' (4 = config 4's 8192 targets per GPU, 5 = config 5, dh7 = the DH arm)")
+                         "under 'legs' (4 = config 4's 8192 targets per GPU, 5 = config 5, dh7 = the DH arm, "
+                         "collide = config 3 with the reference's collider boxes)")
     ap.add_argument("--extra-steps", type=int, default=2, help="timed steps per extra leg (0 = no extra legs)")
     ap.add_argument("--extra-warmup", type=int, default=1)
+    ap.add_argument("--frames", type=int, default=100,
+                    help="with config 3: median wall time of this many consecutive visualiser calls (calculatePSO, "
+                         "N = 16384, 15 iterations), FAST and REFERENCE (0 = skip)")
     ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
                     help="gloo: rehearse the N>1 path with ranks sharing the visible GPUs (not a measurement)")
     return ap.parse_args()
@@ -193,7 +200,8 @@ def cpu_baseline(seconds: float, threads: int, dh=None):
         dd, ed = _cpu_sample(oracle, lib, dh, dh.particles, 50, 0, threads, seconds / 2, 16, kwd)
         dhres = {"value": dd * dh.particles * 50 / ed, "unit": "particle-updates/s", "cores": threads,
                  "sample": f"{dd} swarms x {dh.particles} particles x 50 iterations of {dh.name}, {ed:.1f} s"}
-    return {"value": ups, "unit": "particle-updates/s", "cores": threads, "kind": "port", "dh": dhres,
+    return {"value": ups, "unit": "particle-updates/s", "cores": threads, "kind": "port", "arith": "reference",
+            "dh": dhres,
             "solves_per_s": done / el, "value_1thread": d1 * P * I / e1, "build": build, **facts,
             "by_threads": {str(n): round(v[0]) for n, v in runs.items()},
             "sample": f"{done} swarms x {P} particles x {I} iterations of config 3 (same targets/seeds), "
@@ -203,12 +211,13 @@ def cpu_baseline(seconds: float, threads: int, dh=None):
                                   f"{e5:.1f} s"}}
 
 
-def timed_leg(ctx, wl, Bl, P, I, steps, warmup, arith="fast", kernel="auto"):
+def timed_leg(ctx, wl, Bl, P, I, steps, warmup, arith="fast", kernel="auto", colliders=None):
     """One workload timed the driver's way on every rank: W untimed steps, then
     K steps between barrier + synchronize on both sides, max over ranks.  A step
     = one batch of Bl swarms per rank (ONE solver launch) + the all-gather of
     the per-swarm results + the copy to the host.  Returns the solver too (the
-    caller closes it)."""
+    caller closes it) and the row count the all-gather returned (checked against
+    the swarms of all ranks)."""
     torch, dist, ikpso, idist, dev, world, rank = (ctx[k] for k in
                                                    ("torch", "dist", "ikpso", "idist", "dev", "world", "rank"))
     import numpy as np
@@ -217,11 +226,12 @@ def timed_leg(ctx, wl, Bl, P, I, steps, warmup, arith="fast", kernel="auto"):
     targets = torch.from_numpy(wl.targets(first, Bl)).to(dev)
     solver = ikpso.BatchSolver(wl.chain, P, pso=ikpso.PSOConfig(0.5, 0.5, 1.25, I), fit=wl.fit, arith=arith,
                                limit_weight=wl.limit_weight, soft_lo=wl.soft_lo, soft_hi=wl.soft_hi,
-                               kernel=kernel, axis_mask=wl.axis_mask, fold=wl.fold)
+                               kernel=kernel, axis_mask=wl.axis_mask, fold=wl.fold, colliders=colliders)
     solver.seed(Bl, seed_base=0, first_swarm=first)
     D = solver.dof
     out = (torch.empty((Bl, D), device=dev), torch.empty((Bl,), device=dev), torch.empty((Bl,), device=dev))
     host = torch.empty((total, D + 2), dtype=torch.float32, pin_memory=True)
+    gathered = []
 
     def step(evs=None):
         if evs is not None:
@@ -232,6 +242,7 @@ def timed_leg(ctx, wl, Bl, P, I, steps, warmup, arith="fast", kernel="auto"):
         rows = idist.pack_results(*out)
         if world > 1:
             rows = idist.gather_rows(rows, total, world)
+        gathered[:] = [int(rows.shape[0])]
         host.copy_(rows, non_blocking=True)
 
     for _ in range(warmup):
@@ -254,9 +265,69 @@ def timed_leg(ctx, wl, Bl, P, I, steps, warmup, arith="fast", kernel="auto"):
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     res = host.numpy()
+    if gathered[0] != total:
+        raise RuntimeError(f"all-gather returned {gathered[0]} rows, expected {total}")
     return {"elapsed": float(t[0]), "kern_ms": float(t[1]), "solver": solver, "D": D, "total": total,
+            "gathered_rows": gathered[0],
             "targets": targets, "first": first, "finite": bool(np.isfinite(res).all()),
             "mean_fitness": float(res[:, D].mean()), "mean_residual": float(res[:, D + 1].mean())}
+
+
+def frame_latency(ikpso, torch, np, arith: str, frames: int = 100):
+    """The visualiser's own call (src/Main.cpp:17,130,222-227): calculatePSO through the
+    reference-compatible entry point with N = 16384 particles and PSOConfig(0.5, 0.5, 1.25, 15),
+    generator states carried across frames, each answer fed back as the next frame's start pose
+    (FromCoords, then ToCUDA).  One warm-up call, then the wall time of `frames` consecutive calls
+    (the call is synchronous on return, like the reference's)."""
+    P, D = 16384, 21
+    old = os.environ.get("IKPSO_ARITH")
+    os.environ["IKPSO_ARITH"] = arith  # the compat entry has no mode argument
+    try:
+        scene = ikpso.reference_scene(reset=True)
+        chain = scene.origin.to_cuda()
+        parts = ikpso.particles_tensor(P, D)
+        bests = torch.zeros(P, dtype=torch.float32, device="cuda")
+        rng = ikpso.rng_tensor(P)
+        if ikpso.init_generators(rng, P) != 0:
+            raise RuntimeError("initGenerators failed")
+        res = np.zeros(D, dtype=np.float32)
+        ts = []
+        for k in range(frames + 1):
+            t0 = time.perf_counter()
+            st = ikpso.calculate_pso(parts, None, bests, rng, P, chain, ikpso.MAIN_PSO, ikpso.MAIN_FITNESS, res)
+            dt = time.perf_counter() - t0
+            if st != 0:
+                raise RuntimeError(f"calculatePSO returned {st}")
+            if k:
+                ts.append(dt)
+            scene.origin.from_coords(res)
+            chain = scene.origin.to_cuda()
+    finally:
+        if old is None:
+            os.environ.pop("IKPSO_ARITH", None)
+        else:
+            os.environ["IKPSO_ARITH"] = old
+    t = np.array(ts) * 1e3
+    return {"frame_ms": round(float(np.median(t)), 4), "p10_ms": round(float(np.percentile(t, 10)), 4),
+            "p90_ms": round(float(np.percentile(t, 90)), 4), "frames": frames, "warmup": 1,
+            "particle_updates_per_s": P * ikpso.MAIN_PSO.iterations / (float(np.median(t)) / 1e3),
+            "residual_after": round(float(scene.check_distance()), 5)}
+
+
+def rank_records(dist, torch, world: int, rank: int, local: int, backend: str):
+    """What the process group itself reports, and every rank's device, gathered to all ranks."""
+    props = torch.cuda.get_device_properties(torch.cuda.current_device())
+    rec = {"rank": rank, "local_rank": local, "host": socket.gethostname(), "pid": os.getpid(),
+           "device": torch.cuda.current_device(), "name": props.name,
+           "pci": "{:04x}:{:02x}:{:02x}".format(getattr(props, "pci_domain_id", 0) or 0,
+                                                getattr(props, "pci_bus_id", 0) or 0,
+                                                getattr(props, "pci_device_id", 0) or 0),
+           "uuid": str(getattr(props, "uuid", "") or "")}
+    if world == 1:
+        return {"world_size": 1, "backend": None, "ranks": [rec]}
+    recs = [None] * world
+    dist.all_gather_object(recs, rec)
+    return {"world_size": dist.get_world_size(), "backend": dist.get_backend(), "ranks": recs}
 
 
 def valu_roofline(kernel: str, ups_launch: float, kern_ms: float, lib_id: str, arith: str = "fast"):
@@ -295,6 +366,37 @@ def valu_roofline(kernel: str, ups_launch: float, kern_ms: float, lib_id: str, a
                     "frac_uniform_cost: transcendentals as 4 slots. stale: the counters were measured on "
                     "another build than the loaded library"}
     return vpu, valu
+
+
+def collide_leg(ctx, steps, warmup, lib_id, plain_ms):
+    """The collider term (src/kernel.cu:104-136): config 3's batch (4096 targets per GPU,
+    1024 particles, 500 iterations) with the reference's initColliders boxes 0 and 3 (src/Main.cpp:537-559:
+    unit cubes at (1,0,0) and (0,0,1), which leave the reset pose clear), and the same collider kernel with
+    the boxes moved 1000 units away (every pair rejected by the sphere test: the term's cost without GJK)."""
+    ikpso = ctx["ikpso"]
+    wl = ikpso.workload(3)
+    boxes = ikpso.init_colliders(4)[[0, 3]]
+    far = boxes.copy()
+    far["pos"] += 1000.0
+    P, I, Bl = wl.particles, wl.iterations, wl.swarms
+    r = timed_leg(ctx, wl, Bl, P, I, steps, warmup, colliders=boxes)
+    rf = timed_leg(ctx, wl, Bl, P, I, 1, 1, colliders=far)
+    _, valu = valu_roofline(r["solver"].kernel + " [colliders]", Bl * P * I, r["kern_ms"], lib_id)
+    st = ROOT / "profiles" / "r05" / "collide_stats.json"
+    leg = {"workload": f"config 3 with initColliders boxes 0 and 3: {wl.description}; {P} particles, {I} iterations",
+           "value": r["total"] * P * I * steps / r["elapsed"], "unit": "particle-updates/s",
+           "solves_per_s": r["total"] * steps / r["elapsed"], "ms_per_step": 1e3 * r["elapsed"] / steps,
+           "kernel_ms": round(r["kern_ms"], 3), "steps": steps, "warmup": warmup, "swarms_per_gpu": Bl,
+           "total_swarms": r["total"], "dof": r["D"], "kernel": r["solver"].kernel,
+           "kernel_ms_far_colliders": round(rf["kern_ms"], 3), "kernel_ms_no_colliders": round(plain_ms, 3),
+           "roofline_frac": valu["frac"] if valu else None,
+           "roofline_stale": valu["stale"] if valu else None,
+           "early_out": json.loads(st.read_text()) if st.exists() else None,
+           "check": {"finite": r["finite"], "mean_fitness": r["mean_fitness"],
+                     "mean_residual": r["mean_residual"]}}
+    r["solver"].close()
+    rf["solver"].close()
+    return leg
 
 
 def extra_leg(ctx, name, steps, warmup, lib_id, cpu=None):
@@ -350,6 +452,7 @@ def main():
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
+    group = rank_records(dist, torch, world, rank, local, args.dist_backend)
     ctx = {"torch": torch, "dist": dist, "ikpso": ikpso, "idist": idist, "dev": dev, "world": world,
            "rank": rank, "backend": args.dist_backend}
 
@@ -373,7 +476,14 @@ def main():
         if isinstance(cfg, str):  # the DH arm's own figure
             cpu = dict(cpu, value=cpu["dh"]["value"], sample=cpu["dh"]["sample"])
 
-    main_leg = timed_leg(ctx, wl, Bl, P, I, args.steps, args.warmup, args.arith, args.kernel)
+    colliders = None
+    if args.colliders != "none":
+        colliders = ikpso.init_colliders(4)
+        if args.colliders == "init03":
+            colliders = colliders[[0, 3]]
+        elif args.colliders == "far4":
+            colliders["pos"] += 1000.0
+    main_leg = timed_leg(ctx, wl, Bl, P, I, args.steps, args.warmup, args.arith, args.kernel, colliders=colliders)
     solver, D, total = main_leg["solver"], main_leg["D"], main_leg["total"]
     elapsed, kern_ms = main_leg["elapsed"], main_leg["kern_ms"]
     targets, first = main_leg["targets"], main_leg["first"]
@@ -381,7 +491,7 @@ def main():
     value = ups_step * args.steps / elapsed
 
     single_ms = None
-    if rank == 0 and cfg != 5:
+    if rank == 0 and cfg != 5 and colliders is None:
         s2 = ikpso.BatchSolver(wl.chain, P, pso=ikpso.PSOConfig(0.5, 0.5, 1.25, I), fit=wl.fit, arith=args.arith,
                                axis_mask=wl.axis_mask, fold=wl.fold)
         s2.seed(1)
@@ -399,7 +509,7 @@ def main():
 
     # the REFERENCE-arithmetic (bit-identical to the oracle) throughput of the same workload, driver-measured
     reference_arith = None
-    if rank == 0 and args.arith == "fast" and args.reference_steps > 0 and cfg in (3, 4):
+    if rank == 0 and args.arith == "fast" and args.reference_steps > 0 and cfg in (3, 4) and colliders is None:
         sr = ikpso.BatchSolver(wl.chain, P, pso=ikpso.PSOConfig(0.5, 0.5, 1.25, I), fit=wl.fit, arith="reference",
                                kernel=args.kernel)
         sr.seed(Bl, seed_base=0, first_swarm=first)
@@ -430,14 +540,21 @@ def main():
                                    "run (tests/test_gpu_trajectory.py); same workload, rank 0"}
         sr.close()
 
+    # the visualiser's own per-frame call (N = 16384, 15 iterations), both arithmetic modes
+    frame = None
+    if rank == 0 and cfg == 3 and args.frames > 0 and colliders is None:
+        frame = {a: frame_latency(ikpso, torch, np, a, args.frames) for a in ("fast", "reference")}
+
     lib_id = ikpso.build_id()
     # the other BASELINE lines, same run and timing rules (every rank): config 4's per-GPU shard, config 5 at
     # its named size, the DH arm -- after the headline legs so the GPU stays busy to the end of the run
     legs = {}
-    if cfg == 3 and args.extra_steps > 0:
+    if cfg == 3 and args.extra_steps > 0 and colliders is None:
         for name in args.extra_legs.split(","):
             name = name.strip()
-            if name:
+            if name == "collide":
+                legs[name] = collide_leg(ctx, args.extra_steps, args.extra_warmup, lib_id, kern_ms)
+            elif name:
                 c5 = cpu.get("config5") if (cpu and name == "5") else None
                 legs["config" + name if name.isdigit() else name] = extra_leg(
                     ctx, name, args.extra_steps, args.extra_warmup, lib_id, c5)
@@ -448,7 +565,8 @@ def main():
         alg_bytes = 20 * D + 8
         alg_gbs = ups_launch * alg_bytes / kern_s / 1e9
         streaming = "streaming" in solver.kernel
-        vpu, valu = valu_roofline(solver.kernel, ups_launch, kern_ms, lib_id, args.arith)
+        vpu, valu = valu_roofline(solver.kernel + (" [colliders]" if colliders is not None else ""), ups_launch,
+                                  kern_ms, lib_id, args.arith)
         # the streaming kernels move x/v/pbest through HBM (HBM-bound); an on-chip kernel without a committed
         # PMC profile is reported unmeasured rather than against the HBM formulation it does not use
         on_chip_unmeasured = not streaming and not valu
@@ -504,16 +622,27 @@ def main():
                             f"{Bl} targets per GPU ({total} total)",
                 "swarms_per_gpu": Bl, "total_swarms": total, "particles": P, "iterations": I, "dof": D,
                 "parallelism": f"dp{world} (swarm shards) + {'RCCL' if args.dist_backend == 'nccl' else 'gloo (rehearsal)'}"
-                               f" all-gather of results" if world > 1
+                               f" all-gather of results; process group: world_size {group['world_size']}, backend "
+                               f"{group['backend']}, {len({r['pci'] + r['host'] for r in group['ranks']})} distinct "
+                               f"devices, {main_leg['gathered_rows']} rows gathered" if world > 1
                 else "1 GPU",
+                "process_group": dict(group, gathered_rows=main_leg["gathered_rows"]),
                 "arith": args.arith,
+                "colliders": args.colliders,
             },
             "solves_per_s": total * args.steps / elapsed,
             "single_solve_ms": single_ms,
             "roofline": roofline,
             "reference_arith": reference_arith,
             "legs": legs or None,
+            "frame": frame,
             "cpu_baseline": cpu,
+            "speedup_vs_cpu": None if not cpu else {
+                "fast": round(value / cpu["value"], 1),
+                "like_for_like": round(reference_arith["value"] / cpu["value"], 1) if reference_arith else None,
+                "note": "fast: the headline (FAST arithmetic) over the CPU oracle (REFERENCE arithmetic); "
+                        "like_for_like: the GPU's REFERENCE-arithmetic leg (bit-identical results) over the same "
+                        "CPU oracle"},
             "build_id": lib_id,
             "check": {"finite": main_leg["finite"], "mean_fitness": main_leg["mean_fitness"],
                       "mean_residual": main_leg["mean_residual"]},

@@ -142,7 +142,11 @@ ikpso_status ikpso_init_generators_seeded(ikpso_rng_state* randoms, int64_t coun
  *   result    [D] floats, any: global-best joint angles (Coordinates).
  *   colliders [collider_count] obj_t, any: boxes of the collider term (src/kernel.cu:104-136):
  *             a particle whose node or link box intersects one (GJK) gets fitness FLT_MAX.
- * Synchronises `stream` before returning. */
+ * Synchronises `stream` before returning.  After the argument checks, an error the
+ * caller's earlier HIP work left pending (unread by hipGetLastError) is returned
+ * (IKPSO_ERR_HIP, ikpso_last_hip_error) and consumed, and nothing runs -- the reference
+ * reports it the same way, from its first cudaGetLastError check
+ * (src/kernel.cu:293-295); ikpso_solve_batch does the same. */
 ikpso_status ikpso_calculate_pso(float* particles, const float* positions, float* bests,
                                  ikpso_rng_state* randoms, int size, const ikpso_node* chain, int node_count,
                                  ikpso_pso_config pso, ikpso_fitness_config fit, float* result,

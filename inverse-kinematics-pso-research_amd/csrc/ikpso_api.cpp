@@ -30,6 +30,32 @@ static_assert(sizeof(ikpso_pso_config) == 16, "PSOConfig is 16 bytes");
 static_assert(sizeof(ikpso_fitness_config) == 12, "FitnessConfig is 12 bytes");
 static_assert(sizeof(ikpso_collider) == 48, "obj_t is 48 bytes");
 
+// Collider-term counters of an IKPSO_COLLIDE_STATS build (tools/collide_stats.py):
+// one device block for the process, read and cleared by ikpso_debug_collide_stats.
+unsigned long long* ikpso::collide_stats_buffer()
+{
+#if IKPSO_COLLIDE_STATS
+    static unsigned long long* buf = nullptr;
+    if (!buf && hipMalloc(&buf, kCsCount * sizeof(unsigned long long)) == hipSuccess)
+        (void)hipMemset(buf, 0, kCsCount * sizeof(unsigned long long));
+    return buf;
+#else
+    return nullptr;
+#endif
+}
+
+#if IKPSO_COLLIDE_STATS
+// [kCsCount] counters since the last reset (reset != 0 clears them after the read).
+extern "C" int ikpso_debug_collide_stats(unsigned long long* out, int reset)
+{
+    unsigned long long* buf = ikpso::collide_stats_buffer();
+    if (!buf) return (int)hipErrorMemoryAllocation;
+    hipError_t e = hipMemcpy(out, buf, ikpso::kCsCount * sizeof(unsigned long long), hipMemcpyDeviceToHost);
+    if (e == hipSuccess && reset) e = hipMemset(buf, 0, ikpso::kCsCount * sizeof(unsigned long long));
+    return (int)e;
+}
+#endif
+
 namespace {
 
 thread_local int g_last_hip_error = 0;
@@ -128,12 +154,11 @@ ikpso_status fetch_any(void* dst, const void* src, size_t bytes)
 {
     if (bytes == 0) return IKPSO_OK;
     // hipPointerGetAttributes reports an unregistered host pointer as an error and
-    // records it as the thread's last error: clear only that one, never a sticky
-    // error the caller's own earlier work left
-    const hipError_t prior = hipPeekAtLastError();
+    // records it as the thread's last error: clear it (the entry points have taken
+    // any error the caller's own earlier work left, take_pending_error)
     hipPointerAttribute_t a{};
     const hipError_t e = hipPointerGetAttributes(&a, src);
-    if (e != hipSuccess && prior == hipSuccess) (void)hipGetLastError();
+    if (e != hipSuccess) (void)hipGetLastError();
     if (e != hipSuccess || a.type == hipMemoryTypeUnregistered) {
         memcpy(dst, src, bytes);
         return IKPSO_OK;
@@ -141,6 +166,14 @@ ikpso_status fetch_any(void* dst, const void* src, size_t bytes)
     IKPSO_HIP(hipMemcpy(dst, src, bytes, hipMemcpyDefault));
     return IKPSO_OK;
 }
+
+// An error the caller's earlier HIP work left pending (not yet read by
+// hipGetLastError) is reported by the next solver call, which then does nothing:
+// the reference's calculatePSO returns it the same way, from its first
+// cudaGetLastError check (src/kernel.cu:293-295).  Taking it here also keeps it from
+// being mistaken for a launch failure of this call (the launches are checked with
+// hipGetLastError).
+hipError_t take_pending_error() { return hipGetLastError(); }
 
 struct Extras {
     const float* positions = nullptr;  // host copy, [4J]
@@ -314,12 +347,33 @@ ikpso_status parse_chain(const std::vector<ikpso_node>& nodes, const ikpso_pso_c
     // aux = [posref 4J | soft_lo 3J | soft_hi 3J | pad to 16 floats | collider records]
     ch.num_coll = ex.collider_count;
     ch.coll_off = ((size_t)10 * J + 15) & ~size_t(15);
-    ch.aux.assign(ch.coll_off + (size_t)16 * ch.num_coll, 0.0f);
+    ch.coll_lim_off = ch.coll_off + (size_t)16 * ch.num_coll;
+    ch.aux.assign(ch.coll_lim_off + (size_t)J * ch.num_coll, 0.0f);
+    // near_collider's limit for node k and collider c (ikpso_collide.h): one sphere around
+    // the node's link box and node box, centred at the link's midpoint, that any box pair
+    // node_collides would test lies within.  Every node position is within
+    // |origin| + sum |len| of the frame's origin (a bound on the exact test's |centre|_1
+    // margin term through |a|_1 <= sqrt(3) |a|).
+    double reach = sqrt((double)ch.m0[3] * ch.m0[3] + (double)ch.m0[7] * ch.m0[7] + (double)ch.m0[11] * ch.m0[11]);
+    for (int k = 1; k <= J; ++k) reach += fabs((double)ch.len[k]);
+    reach *= 1.001;
+    const double gb = (double)kGainBound, lw = (double)kGizmo * 0.25;
+    const double rn = 0.5 * sqrt(3.0) * (double)kGizmo * gb;
     for (int i = 0; i < ch.num_coll; ++i) {
         const CollRec r = collider_record(ex.colliders[i]);
         memcpy(ch.aux.data() + ch.coll_off + 16 * (size_t)i, &r, sizeof(r));
         if (!std::isfinite(r.radius) || !std::isfinite(r.px) || !std::isfinite(r.py) || !std::isfinite(r.pz))
             return IKPSO_ERR_INVALID_ARG;
+        const double c1 = fabs((double)r.px) + fabs((double)r.py) + fabs((double)r.pz);
+        for (int k = 1; k <= J; ++k) {
+            const double len = fabs((double)ch.len[k]);
+            const double rl = 0.5 * sqrt(len * len + 2.0 * lw * lw) * gb;
+            const double rk = std::max(rl, 0.5 * len * 1.00001 + rn);
+            const double reach_kc = rk + (double)r.radius;
+            const double lim = (reach_kc + 1e-3 + 1e-4 * (sqrt(3.0) * reach + c1 + reach_kc)) * 1.0001;
+            if (!std::isfinite(lim)) return IKPSO_ERR_INVALID_ARG;
+            ch.aux[ch.coll_lim_off + (size_t)(k - 1) * ch.num_coll + i] = (float)(lim * lim);
+        }
     }
     if (ch.use_posref && ex.positions)
         for (int i = 0; i < 4 * J; ++i) ch.aux[i] = ex.positions[i + (ex.posref_node_slot ? 8 : 0)];
@@ -515,15 +569,16 @@ ikpso_status scratch(size_t bytes, float** out)
     return IKPSO_OK;
 }
 
-// True when `p` is device memory (a kernel writes it directly; anything else --
-// pageable, pinned or managed host memory -- gets the answer through the pinned block).
+// True when `p` is memory of the current device (a kernel writes it directly;
+// anything else -- pageable, pinned or managed host memory, another GPU's memory --
+// gets the answer through the pinned block and a copy).
 bool is_device_memory(const void* p)
 {
-    const hipError_t prior = hipPeekAtLastError();
     hipPointerAttribute_t a{};
     const hipError_t e = hipPointerGetAttributes(&a, p);
-    if (e != hipSuccess && prior == hipSuccess) (void)hipGetLastError();  // see fetch_any
-    return e == hipSuccess && a.type == hipMemoryTypeDevice;
+    if (e != hipSuccess) (void)hipGetLastError();  // our own lookup's error (see fetch_any)
+    int cur = -1;
+    return e == hipSuccess && a.type == hipMemoryTypeDevice && hipGetDevice(&cur) == hipSuccess && a.device == cur;
 }
 
 // Carve 256-byte aligned arrays out of one allocation.
@@ -805,6 +860,7 @@ ikpso_status ikpso_calculate_pso(float* particles, const float* positions, float
     if (size <= 0 || !particles || !bests || !randoms || !chain || !result || node_count < 2 ||
         node_count - 1 > kMaxJoints || pso.iterations < 0)
         return IKPSO_ERR_INVALID_ARG;
+    IKPSO_HIP(take_pending_error());
     std::vector<ikpso_node> nodes(node_count);
     ikpso_status st = fetch_any(nodes.data(), chain, sizeof(ikpso_node) * node_count);
     if (st != IKPSO_OK) return st;
@@ -878,7 +934,10 @@ ikpso_status ikpso_calculate_pso(float* particles, const float* positions, float
     const bool direct = is_device_memory(result);
     float* const out = direct ? result : reinterpret_cast<float*>(g_frame.pinned_dev + 64);
     const hipStream_t s = (hipStream_t)stream;
-    if (g_frame.aux_at != dres + aux_at || g_frame.aux != ch.aux) {
+    // the cached block is compared byte for byte (a value comparison would take -0 for +0 and
+    // never match a NaN)
+    if (g_frame.aux_at != dres + aux_at || g_frame.aux.size() != ch.aux.size() ||
+        (!ch.aux.empty() && memcmp(g_frame.aux.data(), ch.aux.data(), sizeof(float) * ch.aux.size()) != 0)) {
         IKPSO_HIP(hipMemcpyAsync(dres + aux_at, ch.aux.data(), sizeof(float) * ch.aux.size(), hipMemcpyHostToDevice, s));
         g_frame.aux_at = dres + aux_at;
         g_frame.aux = ch.aux;
@@ -1085,6 +1144,7 @@ ikpso_status ikpso_solve_batch(ikpso_solver* s, const float* targets, const floa
     if (!out_angles) return IKPSO_ERR_INVALID_ARG;  // targets == NULL: chain targets for every swarm
     if (num_swarms > s->capacity || !s->rng) return IKPSO_ERR_INVALID_ARG;  // seed first
     if (num_swarms > 0x7fffffff) return IKPSO_ERR_INVALID_ARG;
+    IKPSO_HIP(take_pending_error());
     const hipStream_t hs = (hipStream_t)stream;
     if (s->pending.active) {  // the previous cooperative solve was not synced: settle it first
         const ikpso_status st = ikpso_solver_sync(s);

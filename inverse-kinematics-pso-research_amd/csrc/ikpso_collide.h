@@ -25,6 +25,12 @@
 // support points, all of which lie inside the two spheres' Minkowski ball --
 // so the early-out never changes the answer, and the (wave-divergent, up to
 // 50-iteration) GJK loop runs only for lanes whose arm is near a collider.
+// The sphere test runs twice: first inline in the fitness, on the node's
+// position and a radius bound that needs no quaternion (near_collider), then --
+// only for lanes near a collider -- out of line with the node's quaternion
+// (node_collides).  A wave whose lanes are all clear of every collider skips the
+// call, whose argument and register save/restore traffic is most of the
+// collider term's cost when nothing is near.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -45,6 +51,37 @@ struct CollRec {
 static_assert(sizeof(CollRec) == 64, "collider record is 16 floats");
 
 constexpr int kGjkIterations = 50;      // GJK_ITERATIONS
+
+// IKPSO_COLLIDE_STATS builds (tools/collide_stats.py; variants/, never shipped)
+// count, per solve, what the collider term does -- lane counts unless noted:
+enum {
+    kCsPre = 0,      // node/collider pairs through the inline sphere test (near_collider)
+    kCsPrePass,      // ... that pass it
+    kCsExact,        // pairs through the quaternion sphere test (node_collides)
+    kCsExactPass,    // ... that pass it (GJK calls)
+    kCsGjkIter,      // GJK loop trips, summed over lanes
+    kCsGjkWaveIter,  // GJK loop trips, summed over waves (what the SIMD executes)
+    kCsGjkHit,       // GJK calls that report an intersection
+    kCsCalls,        // node_collides calls, summed over waves
+    kCsCount
+};
+#ifndef IKPSO_COLLIDE_STATS
+#define IKPSO_COLLIDE_STATS 0
+#endif
+#if IKPSO_COLLIDE_STATS
+#define IKPSO_CS_PARAM , unsigned long long* cs
+#define IKPSO_CS_ARG , cs
+// add the number of active lanes with `pred` to counter i (one atomic per wave)
+__device__ __forceinline__ void cs_count(unsigned long long* cs, int i, bool pred)
+{
+    const unsigned long long active = __builtin_amdgcn_read_exec();
+    const unsigned long long m = __builtin_amdgcn_ballot_w64(pred);
+    if (cs && (int)__lane_id() == __builtin_ctzll(active)) atomicAdd(&cs[i], (unsigned long long)__builtin_popcountll(m));
+}
+#else
+#define IKPSO_CS_PARAM
+#define IKPSO_CS_ARG
+#endif
 constexpr float kGizmo = 0.2f;          // GIZMO_SIZE
 
 struct V3 {
@@ -241,7 +278,7 @@ __device__ __forceinline__ int simplex3(V3& s0, V3& s1, V3& s2, int& n, V3& dir)
 }
 
 // GJKIntersect (src/kernel.cu:532-592): true if the boxes intersect.
-__device__ __noinline__ bool gjk_intersect(Box a, Box b)
+__device__ __noinline__ bool gjk_intersect(Box a, Box b IKPSO_CS_PARAM)
 {
     V3 dir = v3(1.0f, 1.0f, 0.0f);  // firstDir
     V3 last = support(a, b, dir);
@@ -249,6 +286,10 @@ __device__ __noinline__ bool gjk_intersect(Box a, Box b)
     int n = 1;
     dir = neg(last);
     for (int it = 0; it < kGjkIterations; ++it) {
+#if IKPSO_COLLIDE_STATS
+        cs_count(cs, kCsGjkIter, true);
+        cs_count(cs, kCsGjkWaveIter, (int)__lane_id() == __builtin_ctzll(__builtin_amdgcn_read_exec()));
+#endif
         last = support(a, b, dir);
         if (dot(last, dir) < 0.0f) return false;
         int r;
@@ -308,6 +349,9 @@ __device__ __noinline__ bool gjk_intersect(Box a, Box b)
                 }
             }
         }
+#if IKPSO_COLLIDE_STATS
+        cs_count(cs, kCsGjkHit, r == 1);
+#endif
         if (r == 1) return true;
         if (r == -1) return false;
         if (is_zero(dot(dir, dir))) return false;
@@ -350,13 +394,58 @@ __device__ __forceinline__ void mat_to_quat(float r00, float r01, float r02, flo
 
 // Sphere test: can the two boxes' support points come within 1e-3?  (The
 // margin also covers the rounding of the support points, ~1e-6 relative.)
-__device__ __forceinline__ bool may_touch(const Box& a, const Box& b)
+__device__ __forceinline__ bool may_touch(float ax, float ay, float az, float ar, float bx, float by, float bz,
+                                          float br)
 {
-    const float dx = a.px - b.px, dy = a.py - b.py, dz = a.pz - b.pz;
-    const float reach = a.radius + b.radius;
-    const float scale_ = fabsf(a.px) + fabsf(a.py) + fabsf(a.pz) + fabsf(b.px) + fabsf(b.py) + fabsf(b.pz) + reach;
+    const float dx = ax - bx, dy = ay - by, dz = az - bz;
+    const float reach = ar + br;
+    const float scale_ = fabsf(ax) + fabsf(ay) + fabsf(az) + fabsf(bx) + fabsf(by) + fabsf(bz) + reach;
     const float lim = reach + 1e-3f + 1e-4f * scale_;
     return dx * dx + dy * dy + dz * dz <= lim * lim;
+}
+__device__ __forceinline__ bool may_touch(const Box& a, const Box& b)
+{
+    return may_touch(a.px, a.py, a.pz, a.radius, b.px, b.py, b.pz, b.radius);
+}
+
+// Bound on quat_gain of a node's quaternion for near_collider, which runs before
+// the quaternion exists.  quat_gain(q) = max(1, sqrt(1 + 4 (|q|^2 - 1) |r|^2)),
+// and matrixToQuaternion of a rotation matrix orthonormal to d gives |q|^2 within
+// ~4d of 1; a node frame is a product of at most 3 x 32 fp32 plane rotations,
+// orthonormal to ~1e-5, so quat_gain <= 1.0001.  1.01 covers |q|^2 up to 1.005,
+// so every pair node_collides would test passes near_collider first.
+constexpr float kGainBound = 1.01f;
+
+// The inline sphere test of node k: may its node box or link box come near a
+// collider?  One sphere around both boxes, centred at the link's midpoint m, per
+// collider c: |m - c|^2 <= lim[k-1][c] -- a limit the host computes from the node's
+// link length, the collider's radius and a bound on the chain's reach so that every
+// pair node_collides would test (its may_touch with the quaternion's gain) passes
+// here first (ikpso_api.cpp: parse_chain).  Three subtractions, a dot product and a
+// compare per collider; no quaternion.
+constexpr int kNearUnroll = 4;
+__device__ __forceinline__ bool near_collider(float nx, float ny, float nz, float ex, float ey, float ez,
+                                              const float* lim, const CollRec* coll, int count IKPSO_CS_PARAM)
+{
+    const float mx = (nx + ex) * 0.5f, my = (ny + ey) * 0.5f, mz = (nz + ez) * 0.5f;
+    bool near = false;
+    auto test = [&](int i) {
+        const CollRec& c = coll[i];
+        const float dx = mx - c.px, dy = my - c.py, dz = mz - c.pz;
+        const bool n = dx * dx + dy * dy + dz * dz <= lim[i];
+#if IKPSO_COLLIDE_STATS
+        cs_count(cs, kCsPre, true);
+        cs_count(cs, kCsPrePass, n);
+#endif
+        near = near || n;
+    };
+    // the first kNearUnroll colliders unrolled under uniform guards (a runtime loop's
+    // back edge made the register allocator spill around it), the rest in a loop
+#pragma unroll
+    for (int i = 0; i < kNearUnroll; ++i)
+        if (i < count) test(i);
+    for (int i = kNearUnroll; i < count; ++i) test(i);
+    return near;
 }
 
 // The collider block of calculateDistance for one node (src/kernel.cu:104-136):
@@ -366,8 +455,12 @@ __device__ __forceinline__ bool may_touch(const Box& a, const Box& b)
 // node of every unrolled chain and runs only on the collider path.
 __device__ __noinline__ bool node_collides(float r00, float r01, float r02, float r10, float r11, float r12,
                                            float r20, float r21, float r22, float nx, float ny, float nz, float ex,
-                                           float ey, float ez, float length, const CollRec* coll, int count)
+                                           float ey, float ez, float length, const CollRec* coll,
+                                           int count IKPSO_CS_PARAM)
 {
+#if IKPSO_COLLIDE_STATS
+    cs_count(cs, kCsCalls, (int)__lane_id() == __builtin_ctzll(__builtin_amdgcn_read_exec()));
+#endif
     float q[4], qi[4];
     mat_to_quat(r00, r01, r02, r10, r11, r12, r20, r21, r22, q);
     quat_inverse(q, qi);
@@ -379,8 +472,16 @@ __device__ __noinline__ bool node_collides(float r00, float r01, float r02, floa
                  qi[3], length, lw, lw, sphere_radius(length, lw, lw, gain)};
     for (int i = 0; i < count; ++i) {
         const Box cb = box_from_record(coll[i]);
-        if (may_touch(nb, cb) && gjk_intersect(nb, cb)) return true;
-        if (may_touch(lb, cb) && gjk_intersect(lb, cb)) return true;
+#if IKPSO_COLLIDE_STATS
+        cs_count(cs, kCsExact, true);
+        cs_count(cs, kCsExactPass, may_touch(nb, cb));
+#endif
+        if (may_touch(nb, cb) && gjk_intersect(nb, cb IKPSO_CS_ARG)) return true;
+#if IKPSO_COLLIDE_STATS
+        cs_count(cs, kCsExact, true);
+        cs_count(cs, kCsExactPass, may_touch(lb, cb));
+#endif
+        if (may_touch(lb, cb) && gjk_intersect(lb, cb IKPSO_CS_ARG)) return true;
     }
     return false;
 }

@@ -303,7 +303,8 @@ __global__ void __launch_bounds__(BLOCK, (kCoopMinWaves<Topo::D, BLOCK, TERMS>))
             const unsigned long long t0 = __builtin_amdgcn_s_memtime();
 #endif
             if constexpr (KA > 0)
-                swarm_step_tip<Topo, MODE, TERMS, BLOCK, KA>(cc, sh, s_pb, tid, x, v, pbf, coef, rng, pa, pc);
+                swarm_step_tip<Topo, MODE, TERMS, BLOCK, KA, !kOwnCU>(cc, sh, s_pb, tid, x, v, pbf, coef, rng, pa,
+                                                                     pc);  // inverted priority: two swarms per CU
             else
                 swarm_step<Topo, MODE, TERMS, BLOCK>(cc, sh, s_pb, tid, x, v, pbf, coef, rng);
             const bool act = cs.member * BLOCK + tid < P;
@@ -748,17 +749,17 @@ inline hipError_t run_coop(const ChainHost& ch, const SwarmIO& io, hipStream_t s
     if constexpr (!Topo::kGeneric && !Topo::kDH && MODE == IKPSO_ARITH_FAST) {
         if constexpr (std::is_same_v<Topo, TopoRef7>) {  // the reference scene's [0, 2pi] limits
             if (terms == kTermUniformBounds && ch.unit_rev_bounds)
-                return launch_coop_kernel<Topo, MODE, kTermUniformBounds | kTermRev | kTermUnitBounds>(cc, io, stream);
+                return launch_coop_kernel<Topo, MODE, kTermUniformBounds | kFastRev | kFastUnitBounds>(cc, io, stream);
         }
         if (terms == kTermUniformBounds)
-            return launch_coop_kernel<Topo, MODE, kTermUniformBounds | kTermRev>(cc, io, stream);
+            return launch_coop_kernel<Topo, MODE, kTermUniformBounds | kFastRev>(cc, io, stream);
         if constexpr (std::is_same_v<Topo, TopoSerialTip<20>>) {  // BASELINE config 5's symmetric soft limits
             if (terms == (kTermUniformBounds | kTermPenalty) && ch.sym_penalty)
-                return launch_coop_kernel<Topo, MODE, kTermUniformBounds | kTermPenalty | kTermRev | kTermSymPenalty>(
+                return launch_coop_kernel<Topo, MODE, kTermUniformBounds | kTermPenalty | kFastRev | kFastSymPenalty>(
                     cc, io, stream);
         }
         if (terms == (kTermUniformBounds | kTermPenalty))
-            return launch_coop_kernel<Topo, MODE, kTermUniformBounds | kTermPenalty | kTermRev>(cc, io, stream);
+            return launch_coop_kernel<Topo, MODE, kTermUniformBounds | kTermPenalty | kFastRev>(cc, io, stream);
     }
     return with_runtime_terms<Topo>(
         ch, [&](auto t) { return launch_coop_kernel<Topo, MODE, decltype(t)::value>(cc, io, stream); });

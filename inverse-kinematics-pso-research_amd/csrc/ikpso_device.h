@@ -138,7 +138,9 @@ __host__ __device__ inline void xorwow_seed(uint64_t seed, uint32_t st[6])
 // TRIG 1 (kTrigHw): the transcendental unit instead (below); TRIG 2 (kTrigHwRev):
 // the same with the angle given in revolutions (kTermRev kernels), so the
 // conversion multiply disappears.
-constexpr int kTrigPoly = 0, kTrigHw = 1, kTrigHwRev = 2;
+// TRIG 3 (kTrigPolyRev): the polynomial on an angle in revolutions (x * 2pi first; only
+// the IKPSO_FAST_HW_TRIG=0 attribution builds).
+constexpr int kTrigPoly = 0, kTrigHw = 1, kTrigHwRev = 2, kTrigPolyRev = 3;
 template <int HW = kTrigPoly>
 __host__ __device__ __forceinline__ void sincos_fast(float x, float* s_out, float* c_out)
 {
@@ -162,6 +164,7 @@ __host__ __device__ __forceinline__ void sincos_fast(float x, float* s_out, floa
         return;
     }
 #endif
+    if constexpr (HW == kTrigPolyRev) x = x * 6.28318530717958648f;
     // Quadrant by the round-to-integer magic constant: k_big = x*2/pi + 1.5*2^23
     // holds q = rint(x*2/pi) in its low mantissa bits (one FMA instead of a
     // multiply, a rint and a float->int conversion); the swap of sin and cos
@@ -193,22 +196,22 @@ __host__ __device__ __forceinline__ void sincos_fast(float x, float* s_out, floa
 }
 
 // REFERENCE: the reduction and the polynomials (fdlibm __kernel_sin /
-// __kernel_cos coefficients) in fp64, rounded once to fp32, so the result is
-// the correctly rounded sinf/cosf except in vanishingly rare near-tie cases --
-// the same property the host libm's double-evaluated sinf/cosf has, which
-// keeps this mode in bitwise agreement with the CPU oracle.
-#ifndef IKPSO_REF_SINCOS_LEAN
-#define IKPSO_REF_SINCOS_LEAN 1
-#endif
+// __kernel_cos coefficients) in fp64, rounded once to fp32.  Equal, bit for bit,
+// to the CPU oracle's (float)sin((double)x) / (float)cos((double)x) on EVERY
+// float with |x| < 4096 (both signs, zeros and subnormals included): checked
+// exhaustively on the host, tests/test_sincos_exhaustive.py.
+//   * the quadrant by the fp64 round-to-integer magic constant (k = rint(x*2/pi):
+//     one fma and one add instead of a multiply, a rint and two conversions);
+//     near a quadrant boundary k may differ by one from the fp32 rint's, the
+//     reduced argument then lies just past pi/4, where the polynomials are as
+//     accurate;
+//   * sin(r) = r * (1 + z*S(z)): the product keeps the sign of r = -0 (the
+//     fma(r*z, S, r) form returned +0 for sin(-0), the one float on which it
+//     differed from the oracle), at the same operation count;
+//   * the quadrant's swap and signs as bit selects on the fp32 results (bitop3 /
+//     xor instead of compares and cndmasks).
 __host__ __device__ __forceinline__ void sincos_reference(float x, float* s_out, float* c_out)
 {
-#if IKPSO_REF_SINCOS_LEAN
-    // The quadrant by the fp64 round-to-integer magic constant (k = rint(x*2/pi):
-    // one fma and one add instead of a multiply, a rint and two conversions), the
-    // quadrant's swap and signs as bit selects on the fp32 results (bitop3 / xor
-    // instead of compares and cndmasks).  Near a quadrant boundary k may differ by
-    // one from the fp32 rint's; the reduced argument then lies just past pi/4,
-    // where the polynomials are as accurate, so the rounded result is the same.
     const double xd = (double)x;
     const double kb = __builtin_fma(xd, 6.36619772367581382433e-01, 6755399441055744.0);  // 1.5 * 2^52 + k
     const double k = kb - 6755399441055744.0;
@@ -223,7 +226,7 @@ __host__ __device__ __forceinline__ void sincos_reference(float x, float* s_out,
     sp = __builtin_fma(z, sp, -1.98412698298579493134e-04);
     sp = __builtin_fma(z, sp, 8.33333333332248946124e-03);
     sp = __builtin_fma(z, sp, -1.66666666666666324348e-01);
-    const double sv = __builtin_fma(r * z, sp, r);
+    const double sv = r * __builtin_fma(z, sp, 1.0);
     double cp = __builtin_fma(z, -1.13596475577881948265e-11, 2.08757232129817482790e-09);
     cp = __builtin_fma(z, cp, -2.75573143513906633035e-07);
     cp = __builtin_fma(z, cp, 2.48015872894767294178e-05);
@@ -242,33 +245,6 @@ __host__ __device__ __forceinline__ void sincos_reference(float x, float* s_out,
     const uint32_t t = q << 30;  // bit 31: q & 2 (sin sign); (q + 1) & 2 for cos
     *s_out = as_float(xor_sign(s1, t));
     *c_out = as_float(xor_sign(c1, t + 0x40000000u));
-#else
-    const float kf = __builtin_rintf(x * 0.636619772367581343f);
-    const double k = (double)kf;
-    double r = __builtin_fma(-k, 1.57079632673412561417e+00, (double)x);
-    r = __builtin_fma(-k, 6.07710050650619224932e-11, r);
-    const double z = r * r;
-    double sp = __builtin_fma(z, 1.58969099521155010221e-10, -2.50507602534068634195e-08);
-    sp = __builtin_fma(z, sp, 2.75573137070700676789e-06);
-    sp = __builtin_fma(z, sp, -1.98412698298579493134e-04);
-    sp = __builtin_fma(z, sp, 8.33333333332248946124e-03);
-    sp = __builtin_fma(z, sp, -1.66666666666666324348e-01);
-    const double sv = __builtin_fma(r * z, sp, r);
-    double cp = __builtin_fma(z, -1.13596475577881948265e-11, 2.08757232129817482790e-09);
-    cp = __builtin_fma(z, cp, -2.75573143513906633035e-07);
-    cp = __builtin_fma(z, cp, 2.48015872894767294178e-05);
-    cp = __builtin_fma(z, cp, -1.38888888888741095749e-03);
-    cp = __builtin_fma(z, cp, 4.16666666666666019037e-02);
-    const double cv = __builtin_fma(z * z, cp, __builtin_fma(-0.5, z, 1.0));
-    const int q = (int)kf;
-    const bool swap = q & 1;
-    float sn = (float)(swap ? cv : sv);
-    float cs = (float)(swap ? sv : cv);
-    sn = (q & 2) ? -sn : sn;
-    cs = ((q + 1) & 2) ? -cs : cs;
-    *s_out = sn;
-    *c_out = cs;
-#endif
 }
 
 // ------------------------------------------------------------- topologies
@@ -573,6 +549,26 @@ constexpr int kTermPosRef = 1, kTermPenalty = 2, kTermRuntime = 4, kTermUniformB
 // free output clamp of |x| - h (<= 1) instead of two subtractions and a v_max3
 // (half rate): BASELINE config 5's +-pi/2 soft limits inside +-pi.
 
+// Parity-attribution builds of FAST arithmetic (tools/tier_b_attribution.py; built into
+// variants/, never shipped): each switch removes one FAST ingredient --
+//   IKPSO_FAST_REV=0            angles in radians (no kTermRev, so no revolution-unit clamp,
+//                               symmetric-penalty clamp or origin-frame FK either);
+//   IKPSO_FAST_HW_TRIG=0        the 1-ulp polynomial instead of v_sin / v_cos;
+//   IKPSO_FAST_TIP_BACKWARD=0   the tip-effector serial chains evaluate their FK forward.
+#ifndef IKPSO_FAST_REV
+#define IKPSO_FAST_REV 1
+#endif
+#ifndef IKPSO_FAST_HW_TRIG
+#define IKPSO_FAST_HW_TRIG 1
+#endif
+#ifndef IKPSO_FAST_TIP_BACKWARD
+#define IKPSO_FAST_TIP_BACKWARD 1
+#endif
+// the revolution-unit terms of the specialised FAST builds (0 in an IKPSO_FAST_REV=0 build)
+constexpr int kFastRev = IKPSO_FAST_REV ? kTermRev : 0;
+constexpr int kFastUnitBounds = IKPSO_FAST_REV ? kTermUnitBounds : 0;
+constexpr int kFastSymPenalty = IKPSO_FAST_REV ? kTermSymPenalty : 0;
+
 // Generator type of a swarm kernel: the add-for-shift issue form everywhere but
 // in the collider kernels, whose register allocation the opaque add perturbs
 // (spills); the draws are bit-identical either way.
@@ -583,11 +579,12 @@ using RngFor = XorwowT<!(TERMS & kTermColliders)>;
 // this topology and term set: chains that run 4 waves per SIMD, no collider term
 // (whose contact decisions the tests compare across kernels bit for bit).
 template <class Topo, int MODE, int TERMS>
-constexpr bool kHwTrigOk = MODE == IKPSO_ARITH_FAST && !(TERMS & kTermColliders) && Topo::D <= 60;
+constexpr bool kHwTrigOk = IKPSO_FAST_HW_TRIG && MODE == IKPSO_ARITH_FAST && !(TERMS & kTermColliders) && Topo::D <= 60;
 // The sin/cos flavour of a kernel build (sincos_fast): polynomial, hardware on
 // radians, or hardware on revolutions (kTermRev).
 template <class Topo, int MODE, int TERMS>
-constexpr int kHwTrig = !kHwTrigOk<Topo, MODE, TERMS> ? kTrigPoly : (TERMS & kTermRev) ? kTrigHwRev : kTrigHw;
+constexpr int kHwTrig = !kHwTrigOk<Topo, MODE, TERMS> ? ((TERMS & kTermRev) ? kTrigPolyRev : kTrigPoly)
+                       : (TERMS & kTermRev) ? kTrigHwRev : kTrigHw;
 template <class Topo, int MODE, int TERMS>
 constexpr bool kRev = (TERMS & kTermRev) != 0;
 // angle / penalty weights of a build (kTermRev: the (2 pi)^2 of the revolution units)
@@ -626,13 +623,18 @@ struct FitnessAcc {
     Frame F[J + 1];
     const float* soft;  // soft limits [lo 3J | hi 3J]: the swarm kernels' LDS copy, else aux in HBM
     float rot_diff, pos_diff, distance, pen;
-    bool hit, posref, penalty;
+    uint32_t near_bits;  // kTermColliders: bit k -- node k's boxes came near a collider (near_collider)
+    // kTermColliders: the frames of the near nodes, for the collider pass -- node k's
+    // world rotation (9), its position and its parent's (6); private memory, written
+    // only for near nodes and read at a runtime index
+    float cfr[(TERMS & kTermColliders) ? J + 1 : 1][15];
+    bool posref, penalty;
 
     // soft_: the soft limits -- pass the swarm kernel's LDS copy (SwarmShared::soft)
     // where there is one: a pointer that may be LDS or global is a flat pointer
     __device__ __forceinline__ FitnessAcc(const ChainConsts<J>& cc, const float*, const float* soft_)
         : soft(soft_), rot_diff(0.0f), pos_diff(0.0f), distance(0.0f), pen(0.0f),
-          hit(false),
+          near_bits(0u),
           posref((TERMS & kTermPosRef) || ((TERMS & kTermRuntime) && cc.use_posref)),
           penalty((TERMS & kTermPenalty) || ((TERMS & kTermRuntime) && cc.use_penalty))
     {
@@ -724,13 +726,24 @@ struct FitnessAcc {
             }
         }
         if constexpr (TERMS & kTermColliders) {
-            // any node/link box hit -> FLT_MAX (the reference returns at the
-            // first hit; later nodes cannot change that).  No colliders: a chain
-            // routed here for its polynomial sin/cos (ChainHost::poly_trig).
-            if (!hit && cc.num_coll > 0)
-                hit = node_collides(F[k].r00, F[k].r01, F[k].r02, F[k].r10, F[k].r11, F[k].r12, F[k].r20, F[k].r21,
-                                    F[k].r22, F[k].px, F[k].py, F[k].pz, F[pk].px, F[pk].py, F[pk].pz, cc.len[k],
-                                    cc.coll, cc.num_coll);
+            // the collider block's inline sphere test on the node's and its parent's
+            // positions; the GJK part runs in finish, for the near nodes only.  No
+            // colliders: a chain routed here for its polynomial sin/cos (ChainHost::poly_trig).
+#if IKPSO_COLLIDE_STATS
+#define IKPSO_CC_STATS , cc.coll_stats
+#else
+#define IKPSO_CC_STATS
+#endif
+            if (cc.num_coll > 0 && near_collider(F[k].px, F[k].py, F[k].pz, F[pk].px, F[pk].py, F[pk].pz,
+                                                 cc.coll_lim + (k - 1) * cc.num_coll, cc.coll, cc.num_coll
+                                                 IKPSO_CC_STATS)) {
+                near_bits |= 1u << k;
+                const float fr[15] = {F[k].r00, F[k].r01, F[k].r02, F[k].r10, F[k].r11, F[k].r12, F[k].r20, F[k].r21,
+                                      F[k].r22, F[k].px,  F[k].py,  F[k].pz,  F[pk].px, F[pk].py, F[pk].pz};
+#pragma unroll
+                for (int i = 0; i < 15; ++i) cfr[k][i] = fr[i];
+            }
+#undef IKPSO_CC_STATS
         }
         if (node_pos) {
             node_pos[3 * (k - 1) + 0] = F[k].px;
@@ -746,13 +759,43 @@ struct FitnessAcc {
         node(cc, k, ang[0], ang[1], ang[2], rest3, tgt3, node_pos);
     }
 
-    __device__ __forceinline__ float finish(const ChainConsts<J>& cc) const
+    // kTermColliders: the collider block (src/kernel.cu:104-136) of the nodes whose
+    // sphere test passed, on the node frames the forward pass kept for them (cfr): any
+    // node or link box hit -> true.  Kept out of the forward pass, so that pass carries
+    // no call (node_collides' caller-saved registers spilled the 1024-lane kernels'
+    // whole iteration to scratch) -- a runtime loop over the near nodes, one call site;
+    // a lane runs it only when one of its nodes came near a collider, a wave only when
+    // one of its lanes did.  The reference returns at the first hit; any hit gives the
+    // same FLT_MAX, so the order does not matter.
+    __device__ __forceinline__ bool collide_pass(const ChainConsts<J>& cc) const
+    {
+#if IKPSO_COLLIDE_STATS
+#define IKPSO_CC_STATS , cc.coll_stats
+#else
+#define IKPSO_CC_STATS
+#endif
+        uint32_t bits = near_bits;
+        bool h = false;
+        while (bits != 0u && !h) {
+            const int k = __builtin_ctz(bits);
+            bits &= bits - 1u;
+            const float* f = cfr[k];
+            h = node_collides(f[0], f[1], f[2], f[3], f[4], f[5], f[6], f[7], f[8], f[9], f[10], f[11], f[12], f[13],
+                              f[14], cc.len[k], cc.coll, cc.num_coll IKPSO_CC_STATS);
+        }
+        return h;
+#undef IKPSO_CC_STATS
+    }
+
+    __device__ __forceinline__ float finish(const ChainConsts<J>& cc, const float* = nullptr) const
     {
 #pragma clang fp contract(off)
         const float aw = angle_weight<TERMS>(cc);
         float f = posref ? (distance + cc.dw_j * pos_diff) + aw * rot_diff : distance + aw * rot_diff;
         if (penalty) f = f + limit_weight<TERMS>(cc) * pen;
-        if constexpr (TERMS & kTermColliders) f = hit ? FLT_MAX : f;
+        if constexpr (TERMS & kTermColliders) {
+            if (near_bits != 0u && collide_pass(cc)) f = FLT_MAX;
+        }
         return f;
     }
 };
@@ -872,7 +915,7 @@ struct FitnessAccDH {
         }
     }
 
-    __device__ __forceinline__ float finish(const ChainConsts<J>& cc) const
+    __device__ __forceinline__ float finish(const ChainConsts<J>& cc, const float* = nullptr) const
     {
         float f = distance + angle_weight<TERMS>(cc) * rot_diff;
         if (penalty) f = f + limit_weight<TERMS>(cc) * pen;
@@ -899,7 +942,7 @@ template <int J>
 struct IsSerialTip<TopoSerialTip<J>> : std::true_type {};
 template <class Topo, int MODE, int TERMS>
 constexpr bool kTipBackward = MODE == IKPSO_ARITH_FAST &&
-                              (IsSerialTip<Topo>::value || Topo::kDH) &&
+                              ((IsSerialTip<Topo>::value && IKPSO_FAST_TIP_BACKWARD) || Topo::kDH) &&
                               !(TERMS & (kTermPosRef | kTermRuntime | kTermColliders | kTermMask));
 
 template <class Topo, int MODE, int TERMS>
@@ -1059,7 +1102,7 @@ __device__ __forceinline__ float fitness(const ChainConsts<Topo::J>& cc, const f
     for (int k = 1; k <= Topo::J; ++k) {
         acc.node(cc, k, x + A * (k - 1), rest + A * (k - 1), tgt + 3 * (k - 1), node_pos);
     }
-    return acc.finish(cc);
+    return acc.finish(cc, x);
 }
 
 // Sum over effectors of the Euclidean distance to target (checkDistance,

@@ -25,6 +25,11 @@
 #define IKPSO_WITH_SERIAL20 1
 #define IKPSO_WITH_OTHERS 0
 #define IKPSO_WITH_DH 0
+#elif defined(IKPSO_EXPERIMENT_REF7_SERIAL20)
+#define IKPSO_WITH_REF7 1
+#define IKPSO_WITH_SERIAL20 1
+#define IKPSO_WITH_OTHERS 0
+#define IKPSO_WITH_DH 0
 #elif defined(IKPSO_EXPERIMENT_DH_ONLY)
 #define IKPSO_WITH_REF7 0
 #define IKPSO_WITH_SERIAL20 0
@@ -52,7 +57,8 @@ struct ChainHost {
     TopoKind topo = TopoKind::Generic;
     std::vector<int> parent, eff_slot;
     std::vector<float> len, eff_w, lo, hi, rest, tgt0;
-    // [posref 4J | soft_lo 3J | soft_hi 3J | collider records 16*num_coll | TopoDH constants] (host copy)
+    // [posref 4J | soft_lo 3J | soft_hi 3J | collider records 16*num_coll | near limits J*num_coll |
+    //  TopoDH constants] (host copy)
     std::vector<float> aux;
     const float* aux_dev = nullptr;  // device copy, owned by the solver / call
     float m0[12] = {};
@@ -64,6 +70,7 @@ struct ChainHost {
     bool sym_penalty = false;     // soft limits symmetric and within a revolution of the clamp (kTermSymPenalty)
     int num_coll = 0;             // colliders (obj_t) of the scene
     size_t coll_off = 0;          // float offset of the collider records in aux
+    size_t coll_lim_off = 0;      // ... of near_collider's squared limits [J][num_coll] (after the records)
     // joint-axis mask over the kernel's dimensions (all set: no mask) and the
     // number of free dimensions, which is the API's D
     uint64_t free_mask = 0;
@@ -134,6 +141,9 @@ __host__ __device__ constexpr int kCoopBlocksPerCU()
 #define IKPSO_SPLIT_QA -1
 #endif
 
+// IKPSO_COLLIDE_STATS builds: the device counters the collider term adds to (null otherwise).
+unsigned long long* collide_stats_buffer();
+
 // Published record of one chunk, in 8-byte granules {value, tag}: the key, then
 // the D floats of the chunk winner's local best; padded to a 128-B multiple.
 __host__ __device__ constexpr int kCoopSlot(int D) { return ((D + 1 + 15) / 16) * 16; }
@@ -190,6 +200,8 @@ ChainConsts<J> make_consts(const ChainHost& h)
     c.num_eff = h.E;
     c.num_coll = h.num_coll;
     c.coll = h.num_coll && h.aux_dev ? reinterpret_cast<const CollRec*>(h.aux_dev + h.coll_off) : nullptr;
+    c.coll_lim = h.num_coll && h.aux_dev ? h.aux_dev + h.coll_lim_off : nullptr;
+    c.coll_stats = collide_stats_buffer();
     c.free_mask = h.free_mask;
     c.dfree = h.dfree;
     c.dh_off = (int32_t)h.dh_off;

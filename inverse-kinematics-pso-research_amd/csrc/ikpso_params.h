@@ -38,6 +38,8 @@ struct ChainConsts {
     int32_t num_eff;
     int32_t num_coll;         // colliders (kTermColliders kernels only)
     const struct CollRec* coll;  // [num_coll] device records, inside the aux buffer
+    const float* coll_lim;    // [J][num_coll] near_collider's squared limits, inside the aux buffer
+    unsigned long long* coll_stats;  // IKPSO_COLLIDE_STATS builds: [kCsCount] counters (else null)
     // Joint-axis mask (extension): bit d set when kernel
     // dimension d is a PSO dimension; dfree = popcount.  The kernels of the
     // Euler topologies run over all 3J Euler angles and honour the mask in their

@@ -129,15 +129,16 @@ __device__ __forceinline__ float swarm_step_ahead(const ChainConsts<Topo::J>& cc
         cur = nxt;
         if (!Topo::kDH) __builtin_amdgcn_sched_barrier(0);
     }
-    return acc.finish(cc);
+    return acc.finish(cc, x);
 }
 
 // Serial chains with a tip effector and the folded chain (kTipBackward
 // builds): all J nodes are updated in dimension order (the same draws; the
 // angle terms in node order), then the tip is evaluated from the tip back
 // (TipAccFor), each node's sines and cosines computed one node ahead of its
-// rotation.
-template <class Topo, int MODE, int TERMS, int BLOCK, int KA = 0, class Rng>
+// rotation.  INV: the inverted wave priority (progress_prio), for the builds
+// whose CU holds workgroups of two different swarms.
+template <class Topo, int MODE, int TERMS, int BLOCK, int KA = 0, bool INV = false, class Rng>
 __device__ __forceinline__ void swarm_step_tip(const ChainConsts<Topo::J>& cc, SwarmShared<Topo>& sh, float* s_pb,
                                                int tid, float (&x)[Topo::D], float (&v)[Topo::D], float& pbf,
                                                const PsoCoef& coef, Rng& rng, const float* pa = nullptr,
@@ -156,7 +157,7 @@ __device__ __forceinline__ void swarm_step_tip(const ChainConsts<Topo::J>& cc, S
     }
 #pragma unroll
     for (int k = 1; k <= J; ++k) {
-        progress_prio<2 * J, PL, (KA > 0)>(k);  // KA > 0: the cooperative build (two swarms per CU)
+        progress_prio<2 * J, PL, INV>(k);
         float cpb[A], cg[A], crest[A];
 #pragma unroll
         for (int ax = 0; ax < A; ++ax) {
@@ -191,7 +192,7 @@ __device__ __forceinline__ void swarm_step_tip(const ChainConsts<Topo::J>& cc, S
     NodeTrig<A> cur = node_trig<Acc::HW, A>(x + A * (J - 1));
 #pragma unroll
     for (int k = J; k >= 1; --k) {
-        progress_prio<2 * J, PL, (KA > 0)>(2 * J + 1 - k);
+        progress_prio<2 * J, PL, INV>(2 * J + 1 - k);
         NodeTrig<A> nxt = cur;
         if (k > 1) nxt = node_trig<Acc::HW, A>(x + A * (k - 2));
         acc.back(cc, k, cur);
@@ -224,7 +225,8 @@ __device__ __forceinline__ void swarm_step(const ChainConsts<Topo::J>& cc, Swarm
         swarm_step_tip<Topo, MODE, TERMS, BLOCK>(cc, sh, s_pb, tid, x, v, pbf, coef, rng);
         return;
     }
-    if constexpr (MODE == IKPSO_ARITH_FAST && Topo::D <= kTrigAheadMaxD) {
+    // (not the collider builds: the pipelined step's extra live node spilled them)
+    if constexpr (MODE == IKPSO_ARITH_FAST && Topo::D <= kTrigAheadMaxD && !(TERMS & kTermColliders)) {
         // updateLocalBests (src/kernel.cu:202-221): strict improvement
         const float f = swarm_step_ahead<Topo, MODE, TERMS, BLOCK>(cc, sh, s_pb, tid, x, v, coef, rng);
         if (f < pbf) {
@@ -246,9 +248,12 @@ __device__ __forceinline__ void swarm_step(const ChainConsts<Topo::J>& cc, Swarm
     for (int c = 0; c < 3; ++c) ntgt[c] = Topo::effector(1) ? sh.tgt[c] : 0.0f;
 #pragma unroll
     for (int k = 1; k <= J; ++k) {
-        // the 2-wave kernels, and (D <= 30: only REFERENCE arithmetic takes this path) the
-        // 4-wave ones: 2 levels, 16.98 -> 15.85 ms on the REFERENCE config-3 shape (2048 x
-        // 1024 x 200, profiles/r04/variant_timings/var_refprio.txt; 3 levels 15.89)
+        // the 2-wave kernels, and the 4-wave ones (D <= 30: only REFERENCE arithmetic takes
+        // this path, FAST takes swarm_step_ahead): 2 levels, 16.98 -> 15.85 ms on the
+        // REFERENCE resident kernel, config-3 shape (2048 x 1024 x 200,
+        // profiles/r04/variant_timings/var_refprio.txt; 3 levels 15.89).  The cooperative
+        // REFERENCE kernels (k_swarm_coop, k_swarm_coop_split) share this step and so the
+        // levelling; they are the parity path and were not timed with and without it.
         progress_prio<J, (D > kTrigAheadMaxD ? kPrioLevels2Wave : kPrioLevels4Wave)>(k);
         float cpb[A], cg[A], crest[A], ctgt[3];
 #pragma unroll
@@ -285,7 +290,7 @@ __device__ __forceinline__ void swarm_step(const ChainConsts<Topo::J>& cc, Swarm
     }
 
     // updateLocalBests (src/kernel.cu:202-221): strict improvement
-    const float f = acc.finish(cc);
+    const float f = acc.finish(cc, x);
     if (f < pbf) {
         pbf = f;
 #pragma unroll
@@ -482,26 +487,26 @@ inline hipError_t run_resident(const ChainHost& ch, const SwarmIO& io, int block
     if constexpr (!Topo::kGeneric && !Topo::kDH && MODE == IKPSO_ARITH_FAST) {
         if constexpr (std::is_same_v<Topo, TopoRef7>) {  // the reference scene's [0, 2pi] limits
             if (terms == kTermUniformBounds && ch.unit_rev_bounds) {
-                hipLaunchKernelGGL((k_swarm_resident<Topo, MODE, kTermUniformBounds | kTermRev | kTermUnitBounds>),
+                hipLaunchKernelGGL((k_swarm_resident<Topo, MODE, kTermUniformBounds | kFastRev | kFastUnitBounds>),
                                    grid, threads, 0, stream, cc, io);
                 return hipGetLastError();
             }
         }
         if (terms == kTermUniformBounds) {
-            hipLaunchKernelGGL((k_swarm_resident<Topo, MODE, kTermUniformBounds | kTermRev>), grid, threads, 0, stream,
+            hipLaunchKernelGGL((k_swarm_resident<Topo, MODE, kTermUniformBounds | kFastRev>), grid, threads, 0, stream,
                                cc, io);
             return hipGetLastError();
         }
         if constexpr (std::is_same_v<Topo, TopoSerialTip<20>>) {  // BASELINE config 5's symmetric soft limits
             if (terms == (kTermUniformBounds | kTermPenalty) && ch.sym_penalty) {
                 hipLaunchKernelGGL(
-                    (k_swarm_resident<Topo, MODE, kTermUniformBounds | kTermPenalty | kTermRev | kTermSymPenalty>),
+                    (k_swarm_resident<Topo, MODE, kTermUniformBounds | kTermPenalty | kFastRev | kFastSymPenalty>),
                     grid, threads, 0, stream, cc, io);
                 return hipGetLastError();
             }
         }
         if (terms == (kTermUniformBounds | kTermPenalty)) {
-            hipLaunchKernelGGL((k_swarm_resident<Topo, MODE, kTermUniformBounds | kTermPenalty | kTermRev>), grid,
+            hipLaunchKernelGGL((k_swarm_resident<Topo, MODE, kTermUniformBounds | kTermPenalty | kFastRev>), grid,
                                threads, 0, stream, cc, io);
             return hipGetLastError();
         }

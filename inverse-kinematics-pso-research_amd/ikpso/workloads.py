@@ -122,10 +122,10 @@ def workload(n) -> Workload:
         P, I, B = {1: (256, 200, 1), 2: (1024, 500, 1), 3: (1024, 500, 4096), 4: (1024, 500, 65536)}[n]
         pso = PSOConfig(0.5, 0.5, 1.25, I)
         desc = {
-            1: "reference scene, reset targets, 256 particles, 200 iterations (CPU plumbing)",
-            2: "reference scene, reset targets, 1024 particles, 500 iterations, 1 swarm",
-            3: "7-joint (21-DOF) reference scene, 4096 perturbed targets, 1024 particles, 500 iterations",
-            4: "as config 3 with 65536 targets sharded over the GPUs",
+            1: "reference scene, reset targets, 1 swarm (CPU plumbing)",
+            2: "reference scene, reset targets, 1 swarm",
+            3: "7-joint (21-DOF) reference scene, perturbed reset targets",
+            4: "7-joint (21-DOF) reference scene, perturbed reset targets, sharded over the GPUs",
         }[n]
         return Workload(f"config{n}", chain, P, I, B, pso, MAIN_FITNESS, description=desc)
     if n == 5:
@@ -135,7 +135,7 @@ def workload(n) -> Workload:
         soft = np.full(D, np.pi / 2, dtype=np.float32)
         return Workload("config5", chain, 4096, 500, 8192, pso, MAIN_FITNESS, limit_weight=10.0, soft_lo=-soft,
                         soft_hi=soft,
-                        description="20-joint serial chain (D=60), tip effector, 4096 particles, 500 iterations, "
+                        description="20-joint serial chain (D=60), tip effector, targets in a radius-2..4 shell, "
                                     "soft joint-limit penalty")
     if isinstance(n, str) and n in ("dh7", "dh7-nofold", "dh7-locked"):
         from .dh import iiwa14
@@ -146,8 +146,8 @@ def workload(n) -> Workload:
                "dh7-nofold": "joint-axis mask (D=7), Euler kernels",
                "dh7-locked": "locked axes by equal clamp bounds (D=33)"}[n]
         return Workload(n, arm.origin.to_cuda(), 1024, 500, 4096, pso, FitnessConfig(0.0, 0.0, 0.1),
-                        description=f"7-joint KUKA iiwa 14 DH arm as 11 nodes, {how}, 4096 reachable targets, "
-                                    "1024 particles, 500 iterations, position-only fitness",
+                        description=f"7-joint KUKA iiwa 14 DH arm as 11 nodes, {how}, reachable targets, "
+                                    "position-only fitness",
                         axis_mask=mask, fold=n == "dh7")
     if isinstance(n, str) and n.isdigit():
         return workload(int(n))

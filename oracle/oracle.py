@@ -67,6 +67,21 @@ def load_native():
     return _NATIVE
 
 
+FMA_PATH = HERE / "_build" / "fma" / "libikpso_oracle.so"
+_FMA = None
+
+
+def load_fma():
+    """The same source with FMA contraction (-mfma -ffp-contract=fast): a second valid
+    fp32 evaluation of every solve, one rounding apart from load()'s -- the tier-B
+    envelope (tests/golden/make_tierb.py)."""
+    global _FMA
+    if _FMA is None:
+        subprocess.run(["make", "-s", "-C", str(HERE), "fma"], check=True)
+        _FMA = _bind(ctypes.CDLL(str(FMA_PATH)))
+    return _FMA
+
+
 def _bind(lib):
     sig = {
         "orc_sizeof_rng": (ctypes.c_int, []),

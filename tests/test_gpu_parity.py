@@ -9,14 +9,16 @@ and residual error"):
   * FAST arithmetic (closed-form FK, FMA, 1-ulp sincos):
       FK/fitness of one pose: |dp| <= 2e-5, |df|/f <= 1e-5
       tier A (I <= 20): |dtheta| <= 1e-4 rad, |df|/f <= 1e-5
-      tier B (I = 200/500, chaotic): per-swarm |df|/f <= 1e-3 for >= 90% of
-      swarms and mean fitness within 0.5%.
+      tier B (I = 200/500, chaotic): the shares of swarms within SURVEY's per-swarm
+      tolerances not lower than the oracle's own FMA on/off envelope (one-sided
+      Fisher exact test), gbest fitness not worse (sign test), both at alpha =
+      0.01 on 256 swarms; mean fitness within 0.5%.
 """
 import numpy as np
 import pytest
 
 import ikpso
-from tierb import tier_b_distances, tier_b_report
+from tierb import envelope, load_fixture, stat_tests, tier_b_distances, tier_b_report
 
 pytestmark = pytest.mark.gpu
 
@@ -184,61 +186,65 @@ def test_tier_b_config1_and_2(oracle, device, scene_chain, monkeypatch):
         assert abs(np.mean(gr) - np.mean(orr)) < 1e-3 + 0.01 * np.mean(orr)
 
 
-TIER_B_SWARMS = 64
-
-
 @pytest.fixture(scope="module")
-def tier_b_case(oracle):
-    """SURVEY.md §8(c) tier B on BASELINE config 3: 64 swarms x 1024 particles x
-    500 iterations, the oracle parallel over the host's cores."""
+def tier_b_case():
+    """SURVEY.md §8(c) tier B on BASELINE config 3: 256 swarms x 1024 particles x
+    500 iterations.  The oracle's answers come from tests/golden/tierb_config3.npz
+    (tests/golden/make_tierb.py; tests/test_tierb_fixtures.py re-solves swarms of it
+    with the oracle bit for bit): `ref`, the parity oracle, and `fma`, the same
+    solves with FMA contraction -- the envelope of two valid fp32 evaluations."""
     wl = ikpso.workload(3)
-    B, P, I = TIER_B_SWARMS, wl.particles, wl.iterations
-    tg = wl.targets(0, B)
-    ostate = oracle.init_generators(B * P, 0)
-    oang, ofit, ores = oracle.solve_batch(wl.chain, tg, None, P, I, ostate, threads=0)
-    return wl, tg, oang, ofit, ores, ostate
+    fx = load_fixture(3)
+    B = int(fx["swarms"])
+    return wl, wl.targets(0, B), fx, envelope(wl.chain, fx)
 
 
 @pytest.mark.parametrize("kernel", ["resident", "auto"])
 @pytest.mark.parametrize("arith", ["fast", "reference"])
 def test_tier_b_config3_batch(oracle, device, tier_b_case, arith, kernel, report):
-    """Tier B on the benchmarked workload, 64 swarms x 1024 x 500, per swarm
-    (|df|/f <= 1e-3, residual within 1e-3, effector positions of
-    the answer within 1e-2 through FK).  After 500 chaotic iterations not every
-    swarm can meet those: two valid fp32 evaluations of the same solve -- the
-    oracle with and without FMA contraction -- meet them on 94 / 91 / 92 % of
-    these swarms, worst swarm 4.0e-2 / 1.4e-2 / 0.21 (tools/tier_b_envelope.py,
-    profiles/r04/tier_b_envelope.json).  So: >= 85 % of swarms within each
-    per-swarm tolerance (>= 90 % for the fitness), mean gbest fitness within
-    0.5 %, mean residual within 1e-3 + 1 %; the generator states after 500
-    iterations bit-exact.  Per-swarm ceilings catch gross errors only: a swarm
-    that settles in another basin moves its residual (a sum of distances to
-    targets the arm cannot all reach; mean 1.75) much further than its fitness
-    -- the GPU measured |dr| up to 0.073 on a swarm whose fitness differs by
-    4 %, the oracle pair 0.014 -- so |df|/f <= 0.1, |dr| <= 0.25, positions <= 0.5.
-    REFERENCE arithmetic: every swarm bit-exact.  AUTO with 64 swarms runs the
-    cooperative latency variant (4 CUs per swarm: config 2's kernel)."""
-    wl, tg, oang, ofit, ores, ostate = tier_b_case
-    B, P, I = TIER_B_SWARMS, wl.particles, wl.iterations
+    """Tier B on the benchmarked workload, per swarm (|df|/f <=
+    1e-3, residual within 1e-3, effector positions of the answer within 1e-2
+    through FK).  After 500 chaotic iterations two valid fp32 evaluations of the
+    same solve -- the oracle with and without FMA contraction -- no longer meet
+    those on every swarm, so the FAST decision is a stated test against that
+    envelope on the same 256 swarms (tests/tierb.py: stat_tests, alpha = 0.01):
+    per tolerance, a one-sided Fisher exact test that the GPU's share of swarms
+    within it is not lower than the envelope's; and a paired sign test that the
+    GPU's gbest fitness is not worse than the oracle's more often than better.
+    Per-swarm ceilings catch gross errors only: no swarm further than twice the
+    envelope's worst swarm on each distance (a swarm settling in another basin
+    moves its residual -- a sum of distances to targets the arm cannot all reach
+    -- much further than its fitness); mean fitness within 0.5 %.  REFERENCE arithmetic: every swarm
+    bit-exact.  Generator states after the solve: bit-exact (D + 3*D*I draws
+    per particle).  AUTO on the first 64 swarms runs the cooperative latency
+    variant (4 CUs per swarm: config 2's kernel)."""
+    wl, tg, fx, env = tier_b_case
+    B = int(fx["swarms"]) if kernel == "resident" else 64
+    P, I, D = wl.particles, wl.iterations, wl.dof
     s = ikpso.BatchSolver(wl.chain, P, pso=wl.pso, arith=arith, kernel=kernel)
     s.seed(B)
-    ang, fit, res = (t.cpu().numpy() for t in s.solve(dev(tg), iterations=I))
+    ang, fit, res = (t.cpu().numpy() for t in s.solve(dev(tg[:B]), iterations=I))
     assert ("latency variant" in s.kernel) == (kernel == "auto"), s.kernel
     states = s.generator_states(0, B)
     s.close()
-    assert np.array_equal(states[:, :6], rng_words(ostate))
+    want = oracle.skipahead(oracle.init_generators(B * P, 0), D + 3 * D * I)
+    assert np.array_equal(states[:, :6], rng_words(want))
+    rang, rfit, rres = fx["ref_angles"][:B], fx["ref_fitness"][:B], fx["ref_residual"][:B]
     if arith == "reference":
-        assert np.array_equal(ang, oang) and np.array_equal(fit, ofit)
+        assert np.array_equal(ang, rang) and np.array_equal(fit, rfit)
         return
-    rel, dres, dpos = tier_b_distances(wl.chain, ang, fit, res, oang, ofit, ores)
-    rep = tier_b_report(rel, dres, dpos)
-    rep.update(mean_fitness=float(fit.mean()), oracle_mean_fitness=float(ofit.mean()), kernel=kernel)
+    dist = tier_b_distances(wl.chain, ang, fit, res, rang, rfit, rres)
+    rep = tier_b_report(*dist)
+    tests = stat_tests(dist, tuple(e[:B] for e in env), fit, rfit)
+    rep.update(mean_fitness=float(fit.mean()), oracle_mean_fitness=float(rfit.mean()), kernel=kernel,
+               envelope=tier_b_report(*(e[:B] for e in env)), tests=tests)
     report(f"tier_b_config3_{kernel}", rep)
-    assert rep["frac_rel_le_1e-3"] >= 0.9, (rep, np.sort(rel)[-8:])
-    assert rep["frac_res_le_1e-3"] >= 0.85 and rep["frac_pos_le_1e-2"] >= 0.85, rep
-    assert rel.max() <= 0.1 and dres.max() <= 0.25 and dpos.max() <= 0.5, rep
-    assert abs(fit.mean() - ofit.mean()) / ofit.mean() < 5e-3
-    assert abs(res.mean() - ores.mean()) < 1e-3 + 0.01 * ores.mean()
+    assert tests["pass"], tests
+    # gross-error ceilings: twice the envelope's worst swarm on the same batch
+    for d, e in zip(dist, env):
+        assert d.max() <= 2 * e[:B].max(), (d.max(), e[:B].max())
+    assert abs(fit.mean() - rfit.mean()) / rfit.mean() < 5e-3
+    assert abs(res.mean() - rres.mean()) < 1e-3 + 0.01 * rres.mean()
 
 
 # --------------------------------------------------------------- tie-breaking
@@ -619,13 +625,15 @@ def test_far_start_pose_inside_narrow_bounds(oracle, device, angle_weight):
     assert np.max(np.abs(fit - ofit) / np.maximum(ofit, 1e-6)) < 1e-4
 
 
-@pytest.mark.parametrize("bounds", [(-1.0, 1.0), (2.0, 1.0), (0.0, 0.0)])
+@pytest.mark.parametrize("bounds", [(-1.0, 1.0), (2.0, 1.0), (0.0, 0.0), (-0.0, 0.0)])
 def test_reference_uniform_bounds_builds(oracle, device, bounds):
     """REFERENCE on the reference tree with uniform clamp bounds: ordered finite
-    bounds take the uniform-bounds build (median clamp, no runtime term tests),
-    inverted ones (lo > hi: the reference's fminf(fmaxf(v, lo), hi) is hi) and
-    degenerate ones the runtime-term build -- every case bit-identical to the
-    oracle (src/matrix_operations.cuh:187-190)."""
+    bounds -- degenerate ones (lo == hi) and signed zeros included -- take the
+    uniform-bounds build (median clamp, no runtime term tests), inverted ones (lo >
+    hi: the reference's fminf(fmaxf(v, lo), hi) is hi) the runtime-term build --
+    every case identical to the oracle byte for byte (src/matrix_operations.cuh:
+    187-190), so a -0 / +0 difference between the median and fminf(fmaxf()) would
+    show."""
     wl = ikpso.workload(3)
     chain = wl.chain.copy()
     chain["min_rotation"][1:] = bounds[0]
@@ -638,4 +646,34 @@ def test_reference_uniform_bounds_builds(oracle, device, bounds):
     s.close()
     ostate = oracle.init_generators(B * P, 0)
     oang, ofit, ores = oracle.solve_batch(chain, tg, None, P, I, ostate, threads=4)
-    assert np.array_equal(ang, oang) and np.array_equal(fit, ofit)
+    assert np.array_equal(ang.view(np.uint32), oang.view(np.uint32))
+    assert np.array_equal(fit.view(np.uint32), ofit.view(np.uint32))
+
+
+def test_pending_caller_error_is_reported_first(device, scene_chain):
+    """An error the caller's earlier HIP work left pending is what calculatePSO
+    returns (and consumes), before it runs anything -- as the reference's first
+    cudaGetLastError check does (src/kernel.cu:293-295); the next call succeeds.
+    A pageable node table (looked up with hipPointerGetAttributes, whose own
+    error the library clears) must not turn a clean call into a failure."""
+    import ctypes
+
+    hip = ctypes.CDLL("libamdhip64.so")
+    P, I = 256, 3
+    parts = ikpso.particles_tensor(P, 21)
+    bests = torch.zeros(P, dtype=torch.float32, device="cuda")
+    rng = ikpso.rng_tensor(P)
+    assert ikpso.init_generators(rng, P) == 0
+    res = np.zeros(21, dtype=np.float32)
+    before = rng.cpu().numpy().copy()
+    assert hip.hipSetDevice(ctypes.c_int(9999)) != 0  # leaves hipErrorInvalidDevice pending
+    st = ikpso.calculate_pso(parts, None, bests, rng, P, scene_chain, ikpso.PSOConfig(0.5, 0.5, 1.25, I),
+                             ikpso.MAIN_FITNESS, res)
+    from ikpso import _abi
+
+    assert st == _abi.IKPSO_ERR_HIP and _abi.load().ikpso_last_hip_error() == 101  # hipErrorInvalidDevice
+    assert np.array_equal(rng.cpu().numpy(), before)  # nothing ran
+    assert hip.hipGetLastError() == 0  # consumed
+    st = ikpso.calculate_pso(parts, None, bests, rng, P, scene_chain, ikpso.PSOConfig(0.5, 0.5, 1.25, I),
+                             ikpso.MAIN_FITNESS, res)
+    assert st == 0

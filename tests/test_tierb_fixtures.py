@@ -1,0 +1,60 @@
+"""The tier-B fixtures (tests/golden/tierb_config{3,5}.npz, made by
+tests/golden/make_tierb.py) against the oracle itself, and the stated tests of
+tests/tierb.py on known inputs.  CPU only."""
+import numpy as np
+import pytest
+
+import ikpso
+from tierb import TOLS, envelope, load_fixture, stat_tests, tier_b_report
+
+
+@pytest.mark.parametrize("cfg,swarms", [(3, [0, 1]), (5, [0])])
+def test_fixture_rows_reproduce(oracle, cfg, swarms):
+    """Re-solve the first swarms of each batch (global seeds: the same streams as in
+    the batch) with both oracle builds: bit-identical to the committed rows."""
+    wl = ikpso.workload(cfg)
+    fx = load_fixture(cfg)
+    B = len(swarms)
+    kw = dict(limit_weight=wl.limit_weight, soft_lo=wl.soft_lo, soft_hi=wl.soft_hi)
+    for name, lib in (("ref", oracle.load()), ("fma", oracle.load_fma())):
+        rng = oracle.init_generators(B * wl.particles, 0)
+        a, f, r = oracle.solve_batch(wl.chain, wl.targets(0, B), None, wl.particles, wl.iterations, rng, lib=lib,
+                                     **kw)
+        assert np.array_equal(a, fx[f"{name}_angles"][swarms]), name
+        assert np.array_equal(f, fx[f"{name}_fitness"][swarms]), name
+        assert np.array_equal(r, fx[f"{name}_residual"][swarms]), name
+
+
+@pytest.mark.parametrize("cfg", [3, 5])
+def test_envelope_is_chaotic_not_broken(cfg):
+    """The FMA-contracted oracle is a valid evaluation: some swarms leave the
+    per-swarm tolerances (chaos), but its fitness is not worse than the parity
+    oracle's and it passes the stated tests against its own envelope."""
+    wl = ikpso.workload(cfg)
+    fx = load_fixture(cfg)
+    env = envelope(wl.chain, fx)
+    rep = tier_b_report(*env)
+    assert rep["swarms"] == int(fx["swarms"]) and rep["swarms"] >= 128
+    assert 0.5 < rep["frac_rel_le_1e-3"] < 1.0  # chaotic, but most swarms agree
+    t = stat_tests(env, env, fx["fma_fitness"], fx["ref_fitness"])
+    assert t["pass"], t
+    assert abs(fx["fma_fitness"].mean() - fx["ref_fitness"].mean()) / fx["ref_fitness"].mean() < 5e-3
+
+
+def test_stat_tests_reject_a_worse_solver():
+    """The tests have power: shares 20 points below the envelope's, or a solver
+    worse on 60 % of 256 swarms, fail at alpha = 0.01."""
+    n = 256
+    rng = np.random.default_rng(5)
+    env = tuple(np.where(rng.random(n) < 0.92, 0.0, 1.0) * tol * 2 for _, tol in TOLS)
+    bad = tuple(np.where(rng.random(n) < 0.72, 0.0, 1.0) * tol * 2 for _, tol in TOLS)
+    ref = rng.uniform(1.0, 2.0, n).astype(np.float32)
+    assert not stat_tests(bad, env, ref, ref)["pass"]
+    worse = ref * np.where(rng.random(n) < 0.6, 1.01, 0.99).astype(np.float32)
+    t = stat_tests(env, env, worse, ref)
+    assert not t["fitness_sign"]["pass"] and t["rel_fitness"]["pass"]
+    assert stat_tests(env, env, ref, ref)["pass"]
+    # a shift inside the ties passes, and shows only in the strict count
+    tiny = (ref.astype(np.float64) * (1 + 2e-6)).astype(np.float32)
+    t = stat_tests(env, env, tiny, ref)
+    assert t["pass"] and t["fitness_sign"]["strict"]["sign_p_worse"] < 0.01

@@ -23,3 +23,66 @@ def tier_b_report(rel, dres, dpos):
     return {"swarms": int(len(rel)), "rel_fitness": q(rel), "residual_abs": q(dres), "effector_pos_abs": q(dpos),
             "frac_rel_le_1e-3": float(np.mean(rel <= 1e-3)), "frac_res_le_1e-3": float(np.mean(dres <= 1e-3)),
             "frac_pos_le_1e-2": float(np.mean(dpos <= 1e-2))}
+
+
+FIXTURE_DIR = __import__("pathlib").Path(__file__).resolve().parent / "golden"
+# SURVEY.md §8(c) tier-B tolerances per swarm: |df|/f, |dr|, effector positions through FK
+TOLS = (("rel_fitness", 1e-3), ("residual_abs", 1e-3), ("effector_pos_abs", 1e-2))
+
+
+def load_fixture(cfg: int) -> dict:
+    """tests/golden/tierb_config{cfg}.npz (tests/golden/make_tierb.py): the oracle's answers
+    (ref: -ffp-contract=off, the parity checker) and the same solves with FMA contraction (fma)."""
+    with np.load(FIXTURE_DIR / f"tierb_config{cfg}.npz") as z:
+        return {k: z[k] for k in z.files}
+
+
+def envelope(chain, fx: dict):
+    """Per-swarm tier-B distances of the FMA-contracted oracle from the parity oracle."""
+    return tier_b_distances(chain, fx["fma_angles"], fx["fma_fitness"], fx["fma_residual"], fx["ref_angles"],
+                            fx["ref_fitness"], fx["ref_residual"])
+
+
+# Ties of the paired fitness comparison: relative differences within 1e-5 -- a hundredth of
+# SURVEY.md §8(c)'s per-swarm fitness tolerance.  The transcendental unit's sin/cos
+# (FAST) round toward zero more often than not (mean amplitude error -3.2e-8,
+# profiles/r05/hwtrig_bias.txt); over config 5's 60 plane rotations that shifts the final
+# fitness by a median +1.4e-6 relative, which a sign test without ties detects
+# (profiles/r05/tier_b_attribution.json reports both).
+SIGN_TIE = 1e-5
+
+
+def stat_tests(dist, env, fit, ref_fit, tie: float = SIGN_TIE):
+    """The FAST-parity decision, stated as tests (alpha = 0.01):
+      * per tolerance of TOLS: one-sided Fisher exact test of H0 "the GPU's share of swarms
+        within the tolerance is at least the envelope's" (two valid fp32 evaluations of the
+        same solves) against "it is lower" -- fails when p < 0.01;
+      * a paired sign test of the per-swarm gbest fitness: H0 "the GPU's answer is as likely
+        better than the oracle's as worse" against "worse", relative differences within
+        `tie` counted as ties -- fails when p < 0.01.  The same test without ties is reported
+        (strict) but not asserted.
+    Returns a report dict with the shares, p-values and verdicts."""
+    from scipy.stats import binomtest, fisher_exact
+
+    out = {}
+    n = len(fit)
+    for (name, tol), d, e in zip(TOLS, dist, env):
+        kg, ke = int(np.sum(d <= tol)), int(np.sum(e <= tol))
+        p = float(fisher_exact([[kg, n - kg], [ke, n - ke]], alternative="less")[1])
+        out[name] = {"tol": tol, "gpu_within": kg, "envelope_within": ke, "swarms": n, "fisher_p_lower": p,
+                     "pass": p >= 0.01}
+
+    def sign(t):
+        rel = (np.asarray(fit, np.float64) - ref_fit) / np.asarray(ref_fit, np.float64)
+        worse, better = int(np.sum(rel > t)), int(np.sum(rel < -t))
+        p = float(binomtest(worse, worse + better, 0.5, alternative="greater").pvalue) if worse + better else 1.0
+        return worse, better, p, float(np.median(rel))
+
+    worse, better, p, med = sign(tie)
+    sw, sb, sp, _ = sign(0.0)
+    out["fitness_sign"] = {"tie": tie, "worse": worse, "better": better, "ties": n - worse - better,
+                           "sign_p_worse": p, "pass": p >= 0.01, "median_rel_diff": med,
+                           "strict": {"worse": sw, "better": sb, "sign_p_worse": sp},
+                           "mean_fitness": float(np.mean(fit)), "oracle_mean_fitness": float(np.mean(ref_fit))}
+    out["pass"] = all(v["pass"] for v in out.values() if isinstance(v, dict))
+    return out

@@ -13,8 +13,9 @@
 #   rocprof      rocprofv3 kernel trace of the default bench command (its average kernel
 #                duration must agree with the line's HIP-event kernel_ms)
 #   profile:<n>  kernel trace + PMC passes (tools/gpu_profile.sh) of workload n in
-#                {c3, c5, dh7, c3ref}: the counters bench.py's roofline reads
+#                {c3, c5, dh7, c3ref, collide}: the counters bench.py's roofline reads
 #   frame        the visualiser frame latency (tools/frame_bench.py)
+#   collstats    collider-term counters (tools/collide_stats.py) with vlib/collide_stats.so
 #   frametrace   rocprofv3 kernel trace of the same (what device work one frame issues)
 #   var:<out>    interleaved variant timing (tools/gpu_var.sh; VAR_ARGS = "CONFIG SWARMS ITERS LIB...")
 #   asan         host-code ASan/UBSan run (tools/asan_check.sh)
@@ -54,9 +55,16 @@ for s in "$@"; do
                    --warmup 1 --cpu-seconds 0 --reference-steps 0 --extra-steps 0" bash tools/gpu_profile.sh || exit 6 ;;
     profile:dh7) PROF_NAME=dh7 PROF_ARGS="--config dh7 --swarms-per-gpu 2048 --steps 2 --warmup 1 --cpu-seconds 0" \
                  bash tools/gpu_profile.sh || exit 6 ;;
+    profile:collide) PROF_NAME=collide PROF_ARGS="--colliders init03 --swarms-per-gpu 2048 --steps 2 --warmup 1 \
+                     --cpu-seconds 0" bash tools/gpu_profile.sh || exit 6 ;;
     profile:c5) PROF_NAME=c5 PROF_ARGS="--config 5 --swarms-per-gpu 2048 --iterations 100 --steps 1 --warmup 1 \
                 --cpu-seconds 0" bash tools/gpu_profile.sh || exit 6 ;;
     frame) step frame 300 python tools/frame_bench.py || exit 7 ;;
+    collstats) [ -f vlib/collide_stats.so ] || { echo "no vlib/collide_stats.so"; exit 10; }
+      for sc in init03 far4 init4; do
+        IKPSO_LIB=vlib/collide_stats.so IKPSO_ALLOW_STALE=1 step "collstats_$sc" 300 \
+          python tools/collide_stats.py ${COLL_SWARMS:-1024} 500 $sc "gpurun_out/collide_stats_$sc.json" || exit 10
+      done ;;
     frametrace)
       step frametrace 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_frame -o run --output-format csv -- \
         python3 tools/frame_bench.py || exit 7 ;;

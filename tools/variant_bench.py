@@ -26,6 +26,34 @@ def open_lib(path):
     return lib
 
 
+def make_solver(lib, wl, P, I, arith="fast", kernel=0):
+    """ikpso_solver_create through `lib` for workload `wl`; returns (handle, arrays to keep alive)."""
+    desc = _abi.SolverDesc()
+    chain = np.ascontiguousarray(wl.chain)
+    desc.chain = chain.ctypes.data
+    desc.node_count = chain.shape[0]
+    desc.particles = P
+    desc.pso = _abi.PSOConfig(0.5, 0.5, 1.25, I)
+    desc.fit = wl.fit.c()
+    desc.arith = 0 if arith == "fast" else 1
+    desc.kernel = kernel
+    keep = [chain]
+    if wl.axis_mask is not None:
+        m = np.ascontiguousarray(wl.axis_mask, np.uint8)
+        keep.append(m)
+        desc.axis_mask = m.ctypes.data
+        desc.flags = 0 if wl.fold else _abi.FLAG_NO_FOLD
+    if wl.limit_weight:
+        lo = np.ascontiguousarray(wl.soft_lo, np.float32)
+        hi = np.ascontiguousarray(wl.soft_hi, np.float32)
+        keep += [lo, hi]
+        desc.limit_weight = wl.limit_weight
+        desc.soft_lo, desc.soft_hi = lo.ctypes.data, hi.ctypes.data
+    h = ctypes.c_void_p()
+    assert lib.ikpso_solver_create(ctypes.byref(desc), ctypes.byref(h)) == 0
+    return h, keep
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("libs", nargs="+")
@@ -45,31 +73,9 @@ def main():
     solvers = []
     for p in a.libs:
         lib = open_lib(p)
-        desc = _abi.SolverDesc()
-        chain = np.ascontiguousarray(wl.chain)
-        desc.chain = chain.ctypes.data
-        desc.node_count = chain.shape[0]
-        desc.particles = P
-        desc.pso = _abi.PSOConfig(0.5, 0.5, 1.25, I)
-        desc.fit = wl.fit.c()
-        desc.arith = 0 if a.arith == "fast" else 1
-        desc.kernel = a.kernel
-        keep = []
-        if wl.axis_mask is not None:
-            m = np.ascontiguousarray(wl.axis_mask, np.uint8)
-            keep.append(m)
-            desc.axis_mask = m.ctypes.data
-            desc.flags = 0 if wl.fold else _abi.FLAG_NO_FOLD
-        if wl.limit_weight:
-            lo = np.ascontiguousarray(wl.soft_lo, np.float32)
-            hi = np.ascontiguousarray(wl.soft_hi, np.float32)
-            keep += [lo, hi]
-            desc.limit_weight = wl.limit_weight
-            desc.soft_lo, desc.soft_hi = lo.ctypes.data, hi.ctypes.data
-        h = ctypes.c_void_p()
-        assert lib.ikpso_solver_create(ctypes.byref(desc), ctypes.byref(h)) == 0
+        h, keep = make_solver(lib, wl, P, I, a.arith, a.kernel)
         assert lib.ikpso_solver_seed(h, B, 0, 0, None) == 0
-        solvers.append((p, lib, h, (chain, keep)))
+        solvers.append((p, lib, h, keep))
     times = {p: [] for p in a.libs}
     results = {}
     for r in range(a.rounds + 1):
