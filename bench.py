@@ -381,7 +381,14 @@ def collide_leg(ctx, steps, warmup, lib_id, plain_ms):
     P, I, Bl = wl.particles, wl.iterations, wl.swarms
     r = timed_leg(ctx, wl, Bl, P, I, steps, warmup, colliders=boxes)
     rf = timed_leg(ctx, wl, Bl, P, I, 1, 1, colliders=far)
-    _, valu = valu_roofline(r["solver"].kernel + " [colliders]", Bl * P * I, r["kern_ms"], lib_id)
+    vpu, valu = valu_roofline(r["solver"].kernel + " [colliders]", Bl * P * I, r["kern_ms"], lib_id)
+    hbm = None
+    if vpu:  # the counter-measured HBM bytes per update: the collider builds' register spills go to HBM
+        gbs = Bl * P * I * vpu["hbm_bytes_per_update"] / (r["kern_ms"] / 1e3) / 1e9
+        hbm = {"achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4),
+               "bytes_per_update": vpu["hbm_bytes_per_update"],
+               "note": "FETCH_SIZE/WRITE_SIZE of the collider kernel: scratch (register spill) traffic, "
+                       "not the algorithm's"}
     st = ROOT / "profiles" / "r05" / "collide_stats.json"
     leg = {"workload": f"config 3 with initColliders boxes 0 and 3: {wl.description}; {P} particles, {I} iterations",
            "value": r["total"] * P * I * steps / r["elapsed"], "unit": "particle-updates/s",
@@ -391,6 +398,7 @@ def collide_leg(ctx, steps, warmup, lib_id, plain_ms):
            "kernel_ms_far_colliders": round(rf["kern_ms"], 3), "kernel_ms_no_colliders": round(plain_ms, 3),
            "roofline_frac": valu["frac"] if valu else None,
            "roofline_stale": valu["stale"] if valu else None,
+           "roofline_hbm": hbm,
            "early_out": json.loads(st.read_text()) if st.exists() else None,
            "check": {"finite": r["finite"], "mean_fitness": r["mean_fitness"],
                      "mean_residual": r["mean_residual"]}}

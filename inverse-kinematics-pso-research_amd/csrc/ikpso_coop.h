@@ -220,11 +220,21 @@ constexpr int kCoopAhead = (kTipBackward<Topo, MODE, TERMS> && Topo::D > 30) ? I
 template <int D, int BLOCK, int TERMS>
 constexpr int kCoopMinWaves = (BLOCK >= 256 ? BLOCK / 256 : 1) *
                               (BLOCK == kCoopThreads<D>() && !(TERMS & kTermColliders) ? kCoopBlocksPerCU<D>() : 1);
+// Pricing builds of a third wave per SIMD for the long chains (variants only): the
+// register budget of three workgroups per CU (168 VGPRs) while LDS still admits two --
+// what the spills alone cost.
+#ifndef IKPSO_EXPERIMENT_COOP_WAVES3
+#define IKPSO_EXPERIMENT_COOP_WAVES3 0
+#endif
+template <int D, int BLOCK, int TERMS>
+constexpr int kCoopBoundWaves =
+    (IKPSO_EXPERIMENT_COOP_WAVES3 && D > 30 && BLOCK == kCoopThreads<D>() && !(TERMS & kTermColliders))
+        ? 3 : kCoopMinWaves<D, BLOCK, TERMS>;
 
 // BLOCK: kCoopThreads<D>() (throughput: fill each CU), or kCoopLatencyThreads
 // for a few swarms (latency: one wave per SIMD on 4x more CUs).
 template <class Topo, int MODE, int TERMS, int BLOCK>
-__global__ void __launch_bounds__(BLOCK, (kCoopMinWaves<Topo::D, BLOCK, TERMS>))
+__global__ void __launch_bounds__(BLOCK, (kCoopBoundWaves<Topo::D, BLOCK, TERMS>))
     k_swarm_coop(const ChainConsts<Topo::J> cc, const SwarmIO io)
 {
     constexpr int J = Topo::J;

@@ -623,18 +623,13 @@ struct FitnessAcc {
     Frame F[J + 1];
     const float* soft;  // soft limits [lo 3J | hi 3J]: the swarm kernels' LDS copy, else aux in HBM
     float rot_diff, pos_diff, distance, pen;
-    uint32_t near_bits;  // kTermColliders: bit k -- node k's boxes came near a collider (near_collider)
-    // kTermColliders: the frames of the near nodes, for the collider pass -- node k's
-    // world rotation (9), its position and its parent's (6); private memory, written
-    // only for near nodes and read at a runtime index
-    float cfr[(TERMS & kTermColliders) ? J + 1 : 1][15];
-    bool posref, penalty;
+    bool hit, posref, penalty;
 
     // soft_: the soft limits -- pass the swarm kernel's LDS copy (SwarmShared::soft)
     // where there is one: a pointer that may be LDS or global is a flat pointer
     __device__ __forceinline__ FitnessAcc(const ChainConsts<J>& cc, const float*, const float* soft_)
         : soft(soft_), rot_diff(0.0f), pos_diff(0.0f), distance(0.0f), pen(0.0f),
-          near_bits(0u),
+          hit(false),
           posref((TERMS & kTermPosRef) || ((TERMS & kTermRuntime) && cc.use_posref)),
           penalty((TERMS & kTermPenalty) || ((TERMS & kTermRuntime) && cc.use_penalty))
     {
@@ -726,23 +721,24 @@ struct FitnessAcc {
             }
         }
         if constexpr (TERMS & kTermColliders) {
-            // the collider block's inline sphere test on the node's and its parent's
-            // positions; the GJK part runs in finish, for the near nodes only.  No
-            // colliders: a chain routed here for its polynomial sin/cos (ChainHost::poly_trig).
+            // any node/link box hit -> FLT_MAX (the reference returns at the first
+            // hit; later nodes cannot change that).  The inline sphere test on the
+            // node's and its parent's positions gates the out-of-line quaternion and
+            // GJK part (node_collides): a wave calls it only when one of its lanes
+            // came near a collider (round 5: 15 % of a wave's nodes on the collide
+            // leg's scene, profiles/r05/collide_stats_init03.json).  No colliders: a
+            // chain routed here for its polynomial sin/cos (ChainHost::poly_trig).
 #if IKPSO_COLLIDE_STATS
 #define IKPSO_CC_STATS , cc.coll_stats
 #else
 #define IKPSO_CC_STATS
 #endif
-            if (cc.num_coll > 0 && near_collider(F[k].px, F[k].py, F[k].pz, F[pk].px, F[pk].py, F[pk].pz,
-                                                 cc.coll_lim + (k - 1) * cc.num_coll, cc.coll, cc.num_coll
-                                                 IKPSO_CC_STATS)) {
-                near_bits |= 1u << k;
-                const float fr[15] = {F[k].r00, F[k].r01, F[k].r02, F[k].r10, F[k].r11, F[k].r12, F[k].r20, F[k].r21,
-                                      F[k].r22, F[k].px,  F[k].py,  F[k].pz,  F[pk].px, F[pk].py, F[pk].pz};
-#pragma unroll
-                for (int i = 0; i < 15; ++i) cfr[k][i] = fr[i];
-            }
+            if (!hit && cc.num_coll > 0 &&
+                near_collider(F[k].px, F[k].py, F[k].pz, F[pk].px, F[pk].py, F[pk].pz,
+                              cc.coll_lim + (k - 1) * cc.num_coll, cc.coll, cc.num_coll IKPSO_CC_STATS))
+                hit = node_collides(F[k].r00, F[k].r01, F[k].r02, F[k].r10, F[k].r11, F[k].r12, F[k].r20, F[k].r21,
+                                    F[k].r22, F[k].px, F[k].py, F[k].pz, F[pk].px, F[pk].py, F[pk].pz, cc.len[k],
+                                    cc.coll, cc.num_coll IKPSO_CC_STATS);
 #undef IKPSO_CC_STATS
         }
         if (node_pos) {
@@ -759,42 +755,14 @@ struct FitnessAcc {
         node(cc, k, ang[0], ang[1], ang[2], rest3, tgt3, node_pos);
     }
 
-    // kTermColliders: the collider block (src/kernel.cu:104-136) of the nodes whose
-    // sphere test passed, on the node frames the forward pass kept for them (cfr): any
-    // node or link box hit -> true.  Kept out of the forward pass, so that pass carries
-    // no call (node_collides' caller-saved registers spilled the 1024-lane kernels'
-    // whole iteration to scratch) -- a runtime loop over the near nodes, one call site;
-    // a lane runs it only when one of its nodes came near a collider, a wave only when
-    // one of its lanes did.  The reference returns at the first hit; any hit gives the
-    // same FLT_MAX, so the order does not matter.
-    __device__ __forceinline__ bool collide_pass(const ChainConsts<J>& cc) const
-    {
-#if IKPSO_COLLIDE_STATS
-#define IKPSO_CC_STATS , cc.coll_stats
-#else
-#define IKPSO_CC_STATS
-#endif
-        uint32_t bits = near_bits;
-        bool h = false;
-        while (bits != 0u && !h) {
-            const int k = __builtin_ctz(bits);
-            bits &= bits - 1u;
-            const float* f = cfr[k];
-            h = node_collides(f[0], f[1], f[2], f[3], f[4], f[5], f[6], f[7], f[8], f[9], f[10], f[11], f[12], f[13],
-                              f[14], cc.len[k], cc.coll, cc.num_coll IKPSO_CC_STATS);
-        }
-        return h;
-#undef IKPSO_CC_STATS
-    }
-
-    __device__ __forceinline__ float finish(const ChainConsts<J>& cc, const float* = nullptr) const
+    __device__ __forceinline__ float finish(const ChainConsts<J>& cc) const
     {
 #pragma clang fp contract(off)
         const float aw = angle_weight<TERMS>(cc);
         float f = posref ? (distance + cc.dw_j * pos_diff) + aw * rot_diff : distance + aw * rot_diff;
         if (penalty) f = f + limit_weight<TERMS>(cc) * pen;
         if constexpr (TERMS & kTermColliders) {
-            if (near_bits != 0u && collide_pass(cc)) f = FLT_MAX;
+            if (hit) f = FLT_MAX;
         }
         return f;
     }
@@ -915,7 +883,7 @@ struct FitnessAccDH {
         }
     }
 
-    __device__ __forceinline__ float finish(const ChainConsts<J>& cc, const float* = nullptr) const
+    __device__ __forceinline__ float finish(const ChainConsts<J>& cc) const
     {
         float f = distance + angle_weight<TERMS>(cc) * rot_diff;
         if (penalty) f = f + limit_weight<TERMS>(cc) * pen;
@@ -1102,7 +1070,7 @@ __device__ __forceinline__ float fitness(const ChainConsts<Topo::J>& cc, const f
     for (int k = 1; k <= Topo::J; ++k) {
         acc.node(cc, k, x + A * (k - 1), rest + A * (k - 1), tgt + 3 * (k - 1), node_pos);
     }
-    return acc.finish(cc, x);
+    return acc.finish(cc);
 }
 
 // Sum over effectors of the Euclidean distance to target (checkDistance,

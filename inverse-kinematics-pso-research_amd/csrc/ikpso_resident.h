@@ -129,7 +129,7 @@ __device__ __forceinline__ float swarm_step_ahead(const ChainConsts<Topo::J>& cc
         cur = nxt;
         if (!Topo::kDH) __builtin_amdgcn_sched_barrier(0);
     }
-    return acc.finish(cc, x);
+    return acc.finish(cc);
 }
 
 // Serial chains with a tip effector and the folded chain (kTipBackward
@@ -290,7 +290,7 @@ __device__ __forceinline__ void swarm_step(const ChainConsts<Topo::J>& cc, Swarm
     }
 
     // updateLocalBests (src/kernel.cu:202-221): strict improvement
-    const float f = acc.finish(cc, x);
+    const float f = acc.finish(cc);
     if (f < pbf) {
         pbf = f;
 #pragma unroll

