@@ -74,7 +74,7 @@ _FMA = None
 def load_fma():
     """The same source with FMA contraction (-mfma -ffp-contract=fast): a second valid
     fp32 evaluation of every solve, one rounding apart from load()'s -- the tier-B
-    envelope (tests/golden/make_tierb.py)."""
+    envelope (tests/golden/make_tierb.py; replaces round 4's tools/tier_b_envelope.py)."""
     global _FMA
     if _FMA is None:
         subprocess.run(["make", "-s", "-C", str(HERE), "fma"], check=True)
