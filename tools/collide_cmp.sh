@@ -1,5 +1,8 @@
+#!/bin/bash
+# Collider-term kernel time at full size (bench.py --colliders {init03,far4}, 4096 x 1024 x 500) for the
+# product library and vlib/ variants, one box: VARIANTS="product coll_vN ..." bash tools/collide_cmp.sh
 mkdir -p gpurun_out
-for v in product coll_v1 coll_v3; do
+for v in ${VARIANTS:-product coll_v1 coll_v3}; do
   for c in init03 far4; do
     if [ $v = product ]; then L=""; else L="IKPSO_LIB=vlib/$v.so IKPSO_ALLOW_STALE=1"; fi
     env $L timeout -k 10 300 python bench.py --colliders $c --steps 2 --warmup 1 --extra-steps 0 --frames 0 --reference-steps 0 --cpu-seconds 0 > gpurun_out/cmp_${v}_$c.log 2>&1 || exit 3
