@@ -25,12 +25,13 @@
 // support points, all of which lie inside the two spheres' Minkowski ball --
 // so the early-out never changes the answer, and the (wave-divergent, up to
 // 50-iteration) GJK loop runs only for lanes whose arm is near a collider.
-// The sphere test runs twice: first inline in the fitness, on the node's
-// position and a radius bound that needs no quaternion (near_collider), then --
-// only for lanes near a collider -- out of line with the node's quaternion
-// (node_collides).  A wave whose lanes are all clear of every collider skips the
-// call, whose argument and register save/restore traffic is most of the
-// collider term's cost when nothing is near.
+// The sphere test runs twice: first inline in the fitness's FK pass, on the
+// node's position and a radius bound that needs no quaternion (near_collider),
+// which keeps the frames of the nodes that pass it; then, after the pass and only
+// for those nodes, out of line with the node's quaternion (node_collides, one call
+// site: FitnessAcc::finish).  node_collides is a leaf function -- GJK and its
+// distance tests inlined at one site -- so a call saves no registers of its own
+// around nested calls.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -201,7 +202,7 @@ __device__ __forceinline__ float point_seg_dist2(V3 P, V3 x0, V3 b, bool witness
 }
 
 // Vec3PointTriDist2 (src/kernel.cu:872-953) with witness == NULL.
-__device__ __noinline__ float point_tri_dist2(V3 P, V3 x0, V3 B, V3 C)
+__device__ __forceinline__ float point_tri_dist2(V3 P, V3 x0, V3 B, V3 C)
 {
     const V3 d1 = B - x0, d2 = C - x0, a = x0 - P;
     const float u = dot(a, a), v = dot(d1, d1), w = dot(d2, d2);
@@ -278,7 +279,7 @@ __device__ __forceinline__ int simplex3(V3& s0, V3& s1, V3& s2, int& n, V3& dir)
 }
 
 // GJKIntersect (src/kernel.cu:532-592): true if the boxes intersect.
-__device__ __noinline__ bool gjk_intersect(Box a, Box b IKPSO_CS_PARAM)
+__device__ __forceinline__ bool gjk_intersect(Box a, Box b IKPSO_CS_PARAM)
 {
     V3 dir = v3(1.0f, 1.0f, 0.0f);  // firstDir
     V3 last = support(a, b, dir);
@@ -451,8 +452,9 @@ __device__ __forceinline__ bool near_collider(float nx, float ny, float nz, floa
 // The collider block of calculateDistance for one node (src/kernel.cu:104-136):
 // node box (GIZMO cube at the node) and link box (length x GIZMO/4 x GIZMO/4,
 // centred between node and parent), both oriented by the node's world
-// rotation, against every collider.  Out of line: it is instantiated once per
-// node of every unrolled chain and runs only on the collider path.
+// rotation, against every collider, in the reference's order (per collider: the
+// node box, then the link box).  Out of line, called from the collider builds'
+// finish() for the near nodes only.
 __device__ __noinline__ bool node_collides(float r00, float r01, float r02, float r10, float r11, float r12,
                                            float r20, float r21, float r22, float nx, float ny, float nz, float ex,
                                            float ey, float ez, float length, const CollRec* coll,
@@ -470,18 +472,18 @@ __device__ __noinline__ bool node_collides(float r00, float r01, float r02, floa
     const float lw = kGizmo * 0.25f;
     const Box lb{(nx + ex) * 0.5f, (ny + ey) * 0.5f, (nz + ez) * 0.5f, q[0], q[1], q[2], q[3], qi[0], qi[1], qi[2],
                  qi[3], length, lw, lw, sphere_radius(length, lw, lw, gain)};
-    for (int i = 0; i < count; ++i) {
-        const Box cb = box_from_record(coll[i]);
+    // one GJK site: pair j = (collider j / 2, node box if j even else link box)
+    for (int j = 0; j < 2 * count; ++j) {
+        const Box cb = box_from_record(coll[j >> 1]);
+        const bool link = j & 1;
+        const Box b{link ? lb.px : nb.px, link ? lb.py : nb.py, link ? lb.pz : nb.pz, nb.qx, nb.qy, nb.qz, nb.qw,
+                    nb.ix, nb.iy, nb.iz, nb.iw, link ? lb.sx : nb.sx, link ? lb.sy : nb.sy, link ? lb.sz : nb.sz,
+                    link ? lb.radius : nb.radius};
 #if IKPSO_COLLIDE_STATS
         cs_count(cs, kCsExact, true);
-        cs_count(cs, kCsExactPass, may_touch(nb, cb));
+        cs_count(cs, kCsExactPass, may_touch(b, cb));
 #endif
-        if (may_touch(nb, cb) && gjk_intersect(nb, cb IKPSO_CS_ARG)) return true;
-#if IKPSO_COLLIDE_STATS
-        cs_count(cs, kCsExact, true);
-        cs_count(cs, kCsExactPass, may_touch(lb, cb));
-#endif
-        if (may_touch(lb, cb) && gjk_intersect(lb, cb IKPSO_CS_ARG)) return true;
+        if (may_touch(b, cb) && gjk_intersect(b, cb IKPSO_CS_ARG)) return true;
     }
     return false;
 }

@@ -617,21 +617,36 @@ template <class Topo, int TERMS>
 constexpr bool kMasked = (TERMS & kTermMask) && !Topo::kDH;
 
 
+#if IKPSO_COLLIDE_STATS
+#define IKPSO_CC_STATS , cc.coll_stats
+#else
+#define IKPSO_CC_STATS
+#endif
 template <class Topo, int MODE, int TERMS>
 struct FitnessAcc {
     static constexpr int J = Topo::J;
     Frame F[J + 1];
     const float* soft;  // soft limits [lo 3J | hi 3J]: the swarm kernels' LDS copy, else aux in HBM
     float rot_diff, pos_diff, distance, pen;
-    bool hit, posref, penalty;
+    bool posref, penalty;
+    // kTermColliders: the nodes whose boxes may touch a collider (bit k-1), and their
+    // frames -- rotation, position, parent position, link length -- for finish(), in
+    // the caller's CandBuf (a separate private array: indexed at run time by finish,
+    // it lives in scratch, and only the near nodes' frames are written to it).
+    // Generic trees test a near node at once (hit): their deferred build hits a
+    // hipcc 7.2 backend error (a flat-to-private check on the buffer's address).
+    static constexpr bool kDefer = (TERMS & kTermColliders) && !Topo::kGeneric;
+    uint32_t near_mask;
+    float* cand;
+    bool hit;
 
     // soft_: the soft limits -- pass the swarm kernel's LDS copy (SwarmShared::soft)
     // where there is one: a pointer that may be LDS or global is a flat pointer
-    __device__ __forceinline__ FitnessAcc(const ChainConsts<J>& cc, const float*, const float* soft_)
+    __device__ __forceinline__ FitnessAcc(const ChainConsts<J>& cc, const float*, const float* soft_, float* cand_)
         : soft(soft_), rot_diff(0.0f), pos_diff(0.0f), distance(0.0f), pen(0.0f),
-          hit(false),
           posref((TERMS & kTermPosRef) || ((TERMS & kTermRuntime) && cc.use_posref)),
-          penalty((TERMS & kTermPenalty) || ((TERMS & kTermRuntime) && cc.use_penalty))
+          penalty((TERMS & kTermPenalty) || ((TERMS & kTermRuntime) && cc.use_penalty)), near_mask(0u),
+          cand(cand_), hit(false)
     {
         F[0] = origin_frame(cc.m0);
     }
@@ -721,25 +736,29 @@ struct FitnessAcc {
             }
         }
         if constexpr (TERMS & kTermColliders) {
-            // any node/link box hit -> FLT_MAX (the reference returns at the first
-            // hit; later nodes cannot change that).  The inline sphere test on the
-            // node's and its parent's positions gates the out-of-line quaternion and
-            // GJK part (node_collides): a wave calls it only when one of its lanes
-            // came near a collider (round 5: 15 % of a wave's nodes on the collide
-            // leg's scene, profiles/r05/collide_stats_init03.json).  No colliders: a
-            // chain routed here for its polynomial sin/cos (ChainHost::poly_trig).
-#if IKPSO_COLLIDE_STATS
-#define IKPSO_CC_STATS , cc.coll_stats
-#else
-#define IKPSO_CC_STATS
-#endif
-            if (!hit && cc.num_coll > 0 &&
-                near_collider(F[k].px, F[k].py, F[k].pz, F[pk].px, F[pk].py, F[pk].pz,
-                              cc.coll_lim + (k - 1) * cc.num_coll, cc.coll, cc.num_coll IKPSO_CC_STATS))
-                hit = node_collides(F[k].r00, F[k].r01, F[k].r02, F[k].r10, F[k].r11, F[k].r12, F[k].r20, F[k].r21,
-                                    F[k].r22, F[k].px, F[k].py, F[k].pz, F[pk].px, F[pk].py, F[pk].pz, cc.len[k],
-                                    cc.coll, cc.num_coll IKPSO_CC_STATS);
-#undef IKPSO_CC_STATS
+            // The inline sphere test on the node's and its parent's positions; a node
+            // that passes it keeps its frame for the quaternion and GJK part, which
+            // finish() runs after the last node (see there).  No colliders: a chain
+            // routed here for its polynomial sin/cos (ChainHost::poly_trig).
+            if (!kDefer) {
+                if (!hit && cc.num_coll > 0 &&
+                    near_collider(F[k].px, F[k].py, F[k].pz, F[pk].px, F[pk].py, F[pk].pz,
+                                  cc.coll_lim + (k - 1) * cc.num_coll, cc.coll, cc.num_coll IKPSO_CC_STATS))
+                    hit = node_collides(F[k].r00, F[k].r01, F[k].r02, F[k].r10, F[k].r11, F[k].r12, F[k].r20,
+                                        F[k].r21, F[k].r22, F[k].px, F[k].py, F[k].pz, F[pk].px, F[pk].py, F[pk].pz,
+                                        cc.len[k], cc.coll, cc.num_coll IKPSO_CC_STATS);
+            } else if (cc.num_coll > 0 &&
+                       near_collider(F[k].px, F[k].py, F[k].pz, F[pk].px, F[pk].py, F[pk].pz,
+                                     cc.coll_lim + (k - 1) * cc.num_coll, cc.coll, cc.num_coll IKPSO_CC_STATS)) {
+                near_mask |= 1u << (k - 1);
+                float* c = cand + 16 * (k - 1);
+                c[0] = F[k].r00, c[1] = F[k].r01, c[2] = F[k].r02;
+                c[3] = F[k].r10, c[4] = F[k].r11, c[5] = F[k].r12;
+                c[6] = F[k].r20, c[7] = F[k].r21, c[8] = F[k].r22;
+                c[9] = F[k].px, c[10] = F[k].py, c[11] = F[k].pz;
+                c[12] = F[pk].px, c[13] = F[pk].py, c[14] = F[pk].pz;
+                c[15] = cc.len[k];
+            }
         }
         if (node_pos) {
             node_pos[3 * (k - 1) + 0] = F[k].px;
@@ -755,6 +774,12 @@ struct FitnessAcc {
         node(cc, k, ang[0], ang[1], ang[2], rest3, tgt3, node_pos);
     }
 
+    // Any node/link box hit -> FLT_MAX (the reference returns at its first hit; a
+    // hit is a hit in any node order).  The quaternion and GJK part (node_collides,
+    // out of line) runs here, once per near node, after the FK pass: a call inside
+    // the pass made every value live across it a spill candidate, and the pass
+    // paid for the spills whether or not a lane came near (round 5: the boxes out
+    // of reach, 214 ms with the call in the pass vs 79 ms without it).
     __device__ __forceinline__ float finish(const ChainConsts<J>& cc) const
     {
 #pragma clang fp contract(off)
@@ -762,7 +787,17 @@ struct FitnessAcc {
         float f = posref ? (distance + cc.dw_j * pos_diff) + aw * rot_diff : distance + aw * rot_diff;
         if (penalty) f = f + limit_weight<TERMS>(cc) * pen;
         if constexpr (TERMS & kTermColliders) {
-            if (hit) f = FLT_MAX;
+            if (hit) f = FLT_MAX;  // (generic trees)
+            uint32_t m = near_mask;
+            while (m != 0u) {
+                const float* c = cand + 16 * __builtin_ctz(m);
+                m &= m - 1u;
+                if (node_collides(c[0], c[1], c[2], c[3], c[4], c[5], c[6], c[7], c[8], c[9], c[10], c[11], c[12],
+                                  c[13], c[14], c[15], cc.coll, cc.num_coll IKPSO_CC_STATS)) {
+                    f = FLT_MAX;
+                    break;
+                }
+            }
         }
         return f;
     }
@@ -790,7 +825,7 @@ struct FitnessAccDH {
     float rot_diff, distance, pen;
     bool penalty;
 
-    __device__ __forceinline__ FitnessAccDH(const ChainConsts<J>& cc, const float* dh, const float* soft_)
+    __device__ __forceinline__ FitnessAccDH(const ChainConsts<J>& cc, const float* dh, const float* soft_, float*)
         : dhc(dh), soft(soft_), rot_diff(0.0f), distance(0.0f), pen(0.0f),
           penalty((TERMS & kTermPenalty) || ((TERMS & kTermRuntime) && cc.use_penalty))
     {
@@ -894,6 +929,11 @@ struct FitnessAccDH {
 template <class Topo, int MODE, int TERMS>
 using FitnessFor =
     std::conditional_t<Topo::kDH, FitnessAccDH<Topo, MODE, TERMS>, FitnessAcc<Topo, MODE, TERMS>>;
+// The near nodes' frames of a FitnessAcc with the collider term (FitnessAcc::cand).
+template <class Topo, int TERMS>
+struct CandBuf {
+    float v[(TERMS & kTermColliders) && !Topo::kDH && !Topo::kGeneric ? 16 * Topo::J : 1];
+};
 
 // FAST serial chains whose only position term is the tip (TopoSerialTip; no
 // distance term, colliders or mask, terms known at compile time): the tip is
@@ -1065,7 +1105,8 @@ __device__ __forceinline__ float fitness(const ChainConsts<Topo::J>& cc, const f
             return tb.finish(cc, tgt + 3 * (J - 1));
         }
     }
-    FitnessFor<Topo, MODE, TERMS> acc(cc, dhc, soft);
+    CandBuf<Topo, TERMS> cb;
+    FitnessFor<Topo, MODE, TERMS> acc(cc, dhc, soft, cb.v);
 #pragma unroll
     for (int k = 1; k <= Topo::J; ++k) {
         acc.node(cc, k, x + A * (k - 1), rest + A * (k - 1), tgt + 3 * (k - 1), node_pos);
@@ -1082,7 +1123,7 @@ __device__ __forceinline__ float residual(const ChainConsts<Topo::J>& cc, const 
 {
     constexpr int J = Topo::J;
     if constexpr (Topo::kDH) {
-        FitnessAccDH<Topo, MODE, TERMS> acc(cc, dhc, cc.aux);  // (no penalty term here)
+        FitnessAccDH<Topo, MODE, TERMS> acc(cc, dhc, cc.aux, nullptr);  // (no penalty term here)
 #pragma unroll
         for (int k = 1; k <= J; ++k) acc.advance(k, x[k - 1]);
         const float dx = tgt[3 * (J - 1) + 0] - acc.px;

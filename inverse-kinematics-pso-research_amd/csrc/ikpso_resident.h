@@ -108,7 +108,8 @@ __device__ __forceinline__ float swarm_step_ahead(const ChainConsts<Topo::J>& cc
 {
     constexpr int J = Topo::J, A = Topo::A;
     constexpr int HW = kHwTrig<Topo, MODE, TERMS>;
-    FitnessFor<Topo, MODE, TERMS> acc(cc, sh.dh, sh.soft);
+    CandBuf<Topo, TERMS> cb;
+    FitnessFor<Topo, MODE, TERMS> acc(cc, sh.dh, sh.soft, cb.v);
     progress_prio<J, kPrioLevels4Wave>(1);
     update_node<Topo, MODE, TERMS, BLOCK>(cc, sh, s_pb, tid, 1, x, v, coef, rng);
     NodeTrig<A> cur = node_trig<HW, A>(x);
@@ -212,9 +213,29 @@ __device__ __forceinline__ void swarm_step_tip(const ChainConsts<Topo::J>& cc, S
     }
 }
 
+// Velocities the resident collider builds keep in LDS, behind the local bests
+// (dimensions 0..kVelLds-1; the rest stay in registers).  node_collides is an
+// out-of-line call (FitnessAcc::finish), and every value live across it that does
+// not fit the callee-saved registers goes to scratch -- around the call and,
+// through the register allocator's choices, on the main path, where a reload of a
+// value spilled an iteration ago comes from HBM.  The velocities are read and
+// written once per iteration: two LDS instructions per dimension.  Round 5, the
+// collide leg's scene (4096 x 1024 x 500): 273 -> 222 ms, and 159 -> 102 ms with
+// the boxes out of reach (profiles/r05/variant_timings/collide_cmp.txt).
+template <class Topo, int TERMS>
+__host__ __device__ constexpr int kVelLds()
+{
+    constexpr int D = Topo::D, BLOCK = kResidentMaxThreads<D>();
+    if (!(TERMS & kTermColliders) || D > 30) return 0;
+    constexpr long spare = 163840L - (long)sizeof(SwarmShared<Topo>) - 256 - (long)D * BLOCK * 4;
+    constexpr long k = spare / (BLOCK * 4);
+    return k <= 0 ? 0 : (k >= D ? D : (int)k);
+}
+
 // Masked chains (kMasked builds): a locked dimension takes no draws and keeps
 // its rest value, as in the oracle's masked restatement.
-template <class Topo, int MODE, int TERMS, int BLOCK, class Rng>
+// KV: velocities held in LDS behind the local bests (kVelLds; the resident kernel)
+template <class Topo, int MODE, int TERMS, int BLOCK, int KV = 0, class Rng>
 __device__ __forceinline__ void swarm_step(const ChainConsts<Topo::J>& cc, SwarmShared<Topo>& sh, float* s_pb,
                                            int tid, float (&x)[Topo::D], float (&v)[Topo::D], float& pbf,
                                            const PsoCoef& coef, Rng& rng)
@@ -236,16 +257,27 @@ __device__ __forceinline__ void swarm_step(const ChainConsts<Topo::J>& cc, Swarm
         }
         return;
     }
-    FitnessFor<Topo, MODE, TERMS> acc(cc, sh.dh, sh.soft);
-    float npb[A], ng[A], nrest[A], ntgt[3];
+    CandBuf<Topo, TERMS> cb;
+    FitnessFor<Topo, MODE, TERMS> acc(cc, sh.dh, sh.soft, cb.v);
+    float* const s_v = s_pb + D * BLOCK;  // KV > 0: velocities [d][lane] (kVelLds)
+    // node kk's local bests, global best, rest angles, target and LDS velocities
+    auto load_node = [&](int kk, float (&pb)[A], float (&g)[A], float (&rest)[A], float (&tgt)[3], float (&vv)[A]) {
 #pragma unroll
-    for (int ax = 0; ax < A; ++ax) {
-        npb[ax] = s_pb[ax * BLOCK + tid];
-        ng[ax] = sh.g[ax];
-        nrest[ax] = sh.rest[ax];
-    }
+        for (int ax = 0; ax < A; ++ax) {
+            const int d = A * (kk - 1) + ax;
+            pb[ax] = s_pb[d * BLOCK + tid];
+            g[ax] = sh.g[d];
+            rest[ax] = sh.rest[d];
+            if (d < KV) vv[ax] = s_v[d * BLOCK + tid];
+        }
 #pragma unroll
-    for (int c = 0; c < 3; ++c) ntgt[c] = Topo::effector(1) ? sh.tgt[c] : 0.0f;
+        for (int c = 0; c < 3; ++c) tgt[c] = Topo::effector(kk) ? sh.tgt[3 * (kk - 1) + c] : 0.0f;
+    };
+    // node k+1's LDS operands are read during node k (also in the collider builds,
+    // where they are live across node_collides' call: reading them at node k instead
+    // measured slower, 181 -> 209 ms with the boxes out of reach)
+    float npb[A], ng[A], nrest[A], ntgt[3], nv[A];
+    load_node(1, npb, ng, nrest, ntgt, nv);
 #pragma unroll
     for (int k = 1; k <= J; ++k) {
         // the 2-wave kernels, and the 4-wave ones (D <= 30: only REFERENCE arithmetic takes
@@ -255,31 +287,27 @@ __device__ __forceinline__ void swarm_step(const ChainConsts<Topo::J>& cc, Swarm
         // REFERENCE kernels (k_swarm_coop, k_swarm_coop_split) share this step and so the
         // levelling; they are the parity path and were not timed with and without it.
         progress_prio<J, (D > kTrigAheadMaxD ? kPrioLevels2Wave : kPrioLevels4Wave)>(k);
-        float cpb[A], cg[A], crest[A], ctgt[3];
+        float cpb[A], cg[A], crest[A], ctgt[3], cv[A];
 #pragma unroll
         for (int ax = 0; ax < A; ++ax) {
             cpb[ax] = npb[ax];
             cg[ax] = ng[ax];
             crest[ax] = nrest[ax];
+            if (A * (k - 1) + ax < KV) cv[ax] = nv[ax];
         }
 #pragma unroll
         for (int c = 0; c < 3; ++c) ctgt[c] = ntgt[c];
-        if (k < J) {
-#pragma unroll
-            for (int ax = 0; ax < A; ++ax) {
-                const int d = A * k + ax;
-                npb[ax] = s_pb[d * BLOCK + tid];
-                ng[ax] = sh.g[d];
-                nrest[ax] = sh.rest[d];
-            }
-#pragma unroll
-            for (int c = 0; c < 3; ++c) ntgt[c] = Topo::effector(k + 1) ? sh.tgt[3 * k + c] : 0.0f;
-        }
+        if (k < J) load_node(k + 1, npb, ng, nrest, ntgt, nv);
 #pragma unroll
         for (int ax = 0; ax < A; ++ax) {
             const int d = A * (k - 1) + ax;
             if (MASK && !dim_free(cc, d)) continue;  // locked: stays at rest
-            pso_update<MODE>(x[d], v[d], cpb[ax], cg[ax], coef, rng);
+            if (d < KV) {
+                pso_update<MODE>(x[d], cv[ax], cpb[ax], cg[ax], coef, rng);
+                s_v[d * BLOCK + tid] = cv[ax];
+            } else {
+                pso_update<MODE>(x[d], v[d], cpb[ax], cg[ax], coef, rng);
+            }
             if constexpr (TERMS & kTermUniformBounds)
                 x[d] = clamp_mode<MODE, true>(x[d], uniform_lo<TERMS>(cc), uniform_hi<TERMS>(cc));
             else
@@ -343,6 +371,10 @@ __device__ __forceinline__ void swarm_resident_body(const ChainConsts<Topo::J>& 
     // initParticlesKernel (src/kernel.cu:223-266)
     float x[D], v[D];
     init_particle<Topo, TERMS, BLOCK>(cc, sh, s_pb, tid, x, v, rng);
+    constexpr int KV = kVelLds<Topo, TERMS>();
+    float* const s_v = s_pb + D * BLOCK;  // (kVelLds)
+#pragma unroll
+    for (int d = 0; d < KV; ++d) s_v[d * BLOCK + tid] = v[d];
     // initLocalBests (src/kernel.cu:191-200)
     float pbf = fitness<Topo, MODE, TERMS>(cc, x, sh.rest, sh.tgt, nullptr, sh.dh, sh.soft);
 
@@ -355,7 +387,7 @@ __device__ __forceinline__ void swarm_resident_body(const ChainConsts<Topo::J>& 
     const PsoCoef coef = pso_coef(cc);
     for (int it = 0; it < io.iterations; ++it) {
         compiler_fence();
-        swarm_step<Topo, MODE, TERMS, BLOCK>(cc, sh, s_pb, tid, x, v, pbf, coef, rng);
+        swarm_step<Topo, MODE, TERMS, BLOCK, KV>(cc, sh, s_pb, tid, x, v, pbf, coef, rng);
 
         // thrust::min_element + `globalMin > currentGlobalMin` (src/kernel.cu:315-323)
         const uint32_t bmin = swarm_argmin(sh, (it + 1) & 1, active ? ordered_key(pbf) : 0xFFFFFFFFu, &bidx);
@@ -384,7 +416,7 @@ __device__ __forceinline__ void swarm_resident_body(const ChainConsts<Topo::J>& 
 #pragma unroll
             for (int d = 0; d < D; ++d) {
                 base[(int64_t)d * P + tid] = radians<TERMS>(x[d]);
-                base[(int64_t)(D + d) * P + tid] = radians<TERMS>(v[d]);
+                base[(int64_t)(D + d) * P + tid] = radians<TERMS>(d < KV ? s_v[d * BLOCK + tid] : v[d]);
                 base[(int64_t)(2 * D + d) * P + tid] = radians<TERMS>(s_pb[d * BLOCK + tid]);
             }
         }
@@ -410,7 +442,8 @@ template <class Topo, int MODE, int TERMS>
 __global__ void __launch_bounds__(kResidentMaxThreads<Topo::D>(), kResidentMinWaves<Topo>)
     k_swarm_resident(const ChainConsts<Topo::J> cc, const SwarmIO io)
 {
-    constexpr int NPB = Topo::D * kResidentMaxThreads<Topo::D>();
+    // local bests [d][lane], then the collider builds' LDS velocities (kVelLds)
+    constexpr int NPB = (Topo::D + kVelLds<Topo, TERMS>()) * kResidentMaxThreads<Topo::D>();
     if constexpr (Topo::kGeneric) {
         // generic trees keep two arrays: hipcc 7.2 miscompiles them over one
         // LDS object (an illegal flat-to-LDS check)

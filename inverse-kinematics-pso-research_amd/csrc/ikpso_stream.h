@@ -169,7 +169,8 @@ __global__ void __launch_bounds__(kStreamChunk) k_stream_step(const ChainConsts<
         // kernels use (swarm_step_tip), so a streaming solve (or a cooperative
         // solve's fallback) rounds like them
         constexpr bool TIP = kTipBackward<Topo, MODE, TERMS>;
-        FitnessFor<Topo, MODE, TERMS> acc(cc, sh.dh, sh.soft);
+        CandBuf<Topo, TERMS> cb;
+        FitnessFor<Topo, MODE, TERMS> acc(cc, sh.dh, sh.soft, cb.v);
         TipAccFor<Topo, MODE, TERMS> tb(sh.dh, sh.soft);
         float xs[TIP ? D : 1];
         // Loads are software-pipelined AHEAD nodes ahead (a ring of AHEAD+1

@@ -69,12 +69,14 @@ def main():
         "gjk_simt_efficiency": c["gjk_lane_trips"] / max(64 * c["gjk_wave_trips"], 1),
         "gjk_hit_rate": c["gjk_hits"] / max(c["exact_pass"], 1),
         "wave_node_call_share": c["wave_calls"] / max(wave_nodes, 1),
+        "calls_per_wave_evaluation": c["wave_calls"] / max(evals // 64, 1),
         "answers_colliding": int((fit > 1e30).sum()),
         "mean_fitness": float(fit[fit < 1e30].mean()) if (fit < 1e30).any() else None,
-        "note": "pre: box/collider pairs through the inline sphere test (node box and link box of every node "
-                "evaluation, until the first hit); exact: pairs through the quaternion test in node_collides, "
-                "called for a lane only when the inline test passed; wave_node_call_share: the share of (wave, "
-                "node) evaluations in which some lane took the call; gjk_simt_efficiency: GJK loop trips summed "
+        "note": "pre: node/collider pairs through the inline sphere test in the FK pass (every node of every "
+                "evaluation); exact: pairs through the quaternion test in node_collides, which the fitness's "
+                "finish calls for the near nodes after the pass, until the first hit; calls_per_wave_evaluation: "
+                "node_collides calls a wave makes per evaluation (one per trip of finish's loop over the lanes' "
+                "near nodes; wave_node_call_share = the same per node); gjk_simt_efficiency: GJK loop trips summed "
                 "over lanes / (64 x trips summed over waves)",
     }
     s.close()
