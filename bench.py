@@ -383,12 +383,13 @@ def collide_leg(ctx, steps, warmup, lib_id, plain_ms):
     rf = timed_leg(ctx, wl, Bl, P, I, 1, 1, colliders=far)
     vpu, valu = valu_roofline(r["solver"].kernel + " [colliders]", Bl * P * I, r["kern_ms"], lib_id)
     hbm = None
-    if vpu:  # the counter-measured HBM bytes per update: the collider builds' register spills go to HBM
+    if vpu:  # the counter-measured HBM bytes per update: the near nodes' stored frames and node_collides' spills
         gbs = Bl * P * I * vpu["hbm_bytes_per_update"] / (r["kern_ms"] / 1e3) / 1e9
         hbm = {"achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4),
                "bytes_per_update": vpu["hbm_bytes_per_update"],
-               "note": "FETCH_SIZE/WRITE_SIZE of the collider kernel: scratch (register spill) traffic, "
-                       "not the algorithm's"}
+               "note": "FETCH_SIZE/WRITE_SIZE of the collider kernel: scratch traffic -- the frames of the nodes "
+                       "near a collider (64 B each, written in the FK pass, read by the GJK pass) and "
+                       "node_collides' register spills"}
     st = ROOT / "profiles" / "r05" / "collide_stats.json"
     leg = {"workload": f"config 3 with initColliders boxes 0 and 3: {wl.description}; {P} particles, {I} iterations",
            "value": r["total"] * P * I * steps / r["elapsed"], "unit": "particle-updates/s",
