@@ -145,3 +145,31 @@ def test_long_chain_colliders_cooperative(oracle, device):
     ostate = oracle.init_generators(B * P, 0)
     oang, ofit, ores = oracle.solve_batch(chain, tg, None, P, I, ostate, colliders=boxes, threads=4)
     assert np.array_equal(ang, oang) and np.array_equal(fit, ofit)
+
+
+@pytest.mark.parametrize("scene,masked", [("all4", False), ("013", False), ("013", True)])
+def test_resident_full_swarm_colliders_reference_bitexact(oracle, device, scene, masked):
+    """The resident collider build at its full 1024 lanes -- the velocities of
+    dimensions 0-17 held in LDS behind the local bests (kVelLds) -- with boxes that
+    the arm reaches: every initColliders box (two intersect the reset pose, so
+    evaluations carry several near nodes and many hit: FitnessAcc::finish's loop over
+    the stored frames runs several trips and stops at a hit), or boxes 0, 1 and 3;
+    unmasked and with an axis mask (the masked collider build).  REFERENCE
+    arithmetic: bit-exact to the oracle."""
+    wl = ikpso.workload(3)
+    boxes = ikpso.init_colliders(4)
+    if scene == "013":
+        boxes = boxes[[0, 1, 3]]
+    mask = np.array([0, 7, 5, 7, 0, 6, 7, 3], np.uint8) if masked else None
+    B, P, I = 3, 1024, 8
+    tg = wl.targets(0, B)
+    s = ikpso.BatchSolver(wl.chain, P, pso=ikpso.PSOConfig(0.5, 0.5, 1.25, I), arith="reference",
+                          kernel="resident", colliders=boxes, axis_mask=mask)
+    assert "resident" in s.kernel
+    s.seed(B)
+    ang, fit, res = (t.cpu().numpy() for t in s.solve(dev(tg), iterations=I))
+    s.close()
+    ostate = oracle.init_generators(B * P, 0)
+    oang, ofit, ores = oracle.solve_batch(wl.chain, tg, None, P, I, ostate, colliders=boxes, threads=8,
+                                          axis_mask=mask)
+    assert np.array_equal(ang, oang) and np.array_equal(fit, ofit)
