@@ -72,12 +72,16 @@ def run_compat(chain, P, I, colliders, seed_base=0):
     return res, parts.cpu().numpy(), bests.cpu().numpy(), r.cpu().numpy()
 
 
-@pytest.mark.parametrize("kernel,P,I", [("resident", 256, 20), ("streaming", 600, 8)])
+@pytest.mark.parametrize("kernel,P,I", [("resident", 256, 20), ("streaming", 600, 8), ("coop", 2048, 6),
+                                      ("auto", 4096, 4)])
 def test_calculate_pso_with_colliders_reference_bitexact(oracle, device, scene_chain, monkeypatch, kernel, P, I):
     """calculatePSO(..., colliders, colliderCount) with colliders 0 and 3 of
     initColliders (1 and 2 intersect the reset pose), REFERENCE arithmetic."""
     monkeypatch.setenv("IKPSO_ARITH", "reference")
-    monkeypatch.setenv("IKPSO_KERNEL", kernel)
+    if kernel != "auto":  # auto: a single swarm of 4096 takes the cooperative latency variant
+        monkeypatch.setenv("IKPSO_KERNEL", kernel)
+    else:
+        monkeypatch.delenv("IKPSO_KERNEL", raising=False)
     boxes = ikpso.init_colliders(4)[[0, 3]]
     res, parts, bests, r = run_compat(scene_chain, P, I, boxes)
     ostate = oracle.init_generators(P, 0)
