@@ -780,7 +780,13 @@ struct FitnessAcc {
     // the pass made every value live across it a spill candidate, and the pass
     // paid for the spills whether or not a lane came near (round 5: the boxes out
     // of reach, 214 ms with the call in the pass vs 79 ms without it).
-    __device__ __forceinline__ float finish(const ChainConsts<J>& cc) const
+    // `pbest`: the caller's local best, when the result only feeds the strict
+    // `f < pbest` update (updateLocalBests, src/kernel.cu:202-221).  A lane whose
+    // collision-free value is already >= a finite pbest cannot improve whether or not
+    // it collides (FLT_MAX is not < pbest either), so it skips the test and returns
+    // that value -- the update, and so every later state, is the same bit for bit.
+    // NaN (the default): every lane is tested, the value is the fitness itself.
+    __device__ __forceinline__ float finish(const ChainConsts<J>& cc, float pbest = __builtin_nanf("")) const
     {
 #pragma clang fp contract(off)
         const float aw = angle_weight<TERMS>(cc);
@@ -788,7 +794,7 @@ struct FitnessAcc {
         if (penalty) f = f + limit_weight<TERMS>(cc) * pen;
         if constexpr (TERMS & kTermColliders) {
             if (hit) f = FLT_MAX;  // (generic trees)
-            uint32_t m = near_mask;
+            uint32_t m = (f >= pbest && pbest <= FLT_MAX) ? 0u : near_mask;
             while (m != 0u) {
                 const float* c = cand + 16 * __builtin_ctz(m);
                 m &= m - 1u;
@@ -918,7 +924,7 @@ struct FitnessAccDH {
         }
     }
 
-    __device__ __forceinline__ float finish(const ChainConsts<J>& cc) const
+    __device__ __forceinline__ float finish(const ChainConsts<J>& cc, float = 0.0f) const  // (no collider term)
     {
         float f = distance + angle_weight<TERMS>(cc) * rot_diff;
         if (penalty) f = f + limit_weight<TERMS>(cc) * pen;

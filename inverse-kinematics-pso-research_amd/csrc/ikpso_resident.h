@@ -318,7 +318,7 @@ __device__ __forceinline__ void swarm_step(const ChainConsts<Topo::J>& cc, Swarm
     }
 
     // updateLocalBests (src/kernel.cu:202-221): strict improvement
-    const float f = acc.finish(cc);
+    const float f = acc.finish(cc, pbf);
     if (f < pbf) {
         pbf = f;
 #pragma unroll

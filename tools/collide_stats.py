@@ -74,7 +74,8 @@ def main():
         "mean_fitness": float(fit[fit < 1e30].mean()) if (fit < 1e30).any() else None,
         "note": "pre: node/collider pairs through the inline sphere test in the FK pass (every node of every "
                 "evaluation); exact: pairs through the quaternion test in node_collides, which the fitness's "
-                "finish calls for the near nodes after the pass, until the first hit; calls_per_wave_evaluation: "
+                "finish calls for the near nodes after the pass -- in the swarm step only for lanes whose collision-free "
+                "value could still improve their local best -- until the first hit; calls_per_wave_evaluation: "
                 "node_collides calls a wave makes per evaluation (one per trip of finish's loop over the lanes' "
                 "near nodes; wave_node_call_share = the same per node); gjk_simt_efficiency: GJK loop trips summed "
                 "over lanes / (64 x trips summed over waves)",
