@@ -439,6 +439,29 @@ def extra_leg(ctx, name, steps, warmup, lib_id, cpu=None):
     return leg
 
 
+def summary(line: dict, value: float) -> dict:
+    """Compact restatement of the line's figures (rounded), printed last."""
+    r3 = lambda x: None if x is None else float(f"{x:.4g}")
+    out = {"value": r3(value), "kernel_ms": line["roofline"].get("kernel_ms"),
+           "roofline_frac": line["roofline"].get("frac"), "single_solve_ms": r3(line.get("single_solve_ms"))}
+    if line.get("frame"):
+        out["frame_ms"] = {a: f["frame_ms"] for a, f in line["frame"].items()}
+    if line.get("reference_arith"):
+        ra = line["reference_arith"]
+        out["reference_arith"] = {"value": r3(ra["value"]), "kernel_ms": ra["kernel_ms"],
+                                  "roofline_frac": ra["roofline_frac"]}
+    for name, leg in (line.get("legs") or {}).items():
+        out[name] = {"value": r3(leg["value"]), "kernel_ms": leg["kernel_ms"], "roofline_frac": leg["roofline_frac"]}
+        for k in ("kernel_ms_far_colliders", "kernel_ms_no_colliders"):
+            if k in leg:
+                out[name][k] = leg[k]
+    cpu = line.get("cpu_baseline")
+    if cpu:
+        out["cpu_baseline"] = {"value": r3(cpu["value"]), "cores": cpu["cores"], "kind": cpu["kind"],
+                               "value_1thread": r3(cpu.get("value_1thread"))}
+    return out
+
+
 def main():
     args = parse()
     launch_ranks(args)
@@ -476,14 +499,19 @@ def main():
     else:
         Bl = -(-wl.swarms // world)         # configs 4/5: the named total over all GPUs
 
-    # the bounded CPU baseline runs before the GPU legs (rank 0, N = 1)
+    # the bounded CPU baseline runs before the GPU legs, on rank 0 at every N (north_star: the CPU path
+    # "alongside" at 1, 2, 4 and 8 GPUs); the other ranks wait for it at a barrier
     cpu = None
-    if rank == 0 and world == 1 and args.cpu_seconds > 0 and cfg in (3, 5, "dh7", "dh7-nofold", "dh7-locked"):
+    if rank == 0 and args.cpu_seconds > 0 and cfg in (3, 5, "dh7", "dh7-nofold", "dh7-locked"):
         cpu = cpu_baseline(args.cpu_seconds, args.cpu_threads, dh=wl if isinstance(cfg, str) else None)
         if cfg == 5:  # the config-5 figure is this line's baseline
             cpu = dict(cpu, value=cpu["config5"]["value"], sample=cpu["config5"]["sample"])
         if isinstance(cfg, str):  # the DH arm's own figure
             cpu = dict(cpu, value=cpu["dh"]["value"], sample=cpu["dh"]["sample"])
+        if world > 1:
+            cpu["note"] = f"rank 0's host cores, timed before the GPU legs while ranks 1..{world - 1} waited"
+    if world > 1:
+        dist.barrier()
 
     colliders = None
     if args.colliders != "none":
@@ -671,6 +699,9 @@ def main():
         if cfg == 2:
             line["roofline"]["note"] = ("config 2 is one swarm on 4 of 256 CUs: latency-bound (SURVEY 8(d)), "
                                         "the chip-wide fraction is not a kernel-quality figure")
+        # the line's last key: the other BASELINE lines in a few hundred bytes, so a reader that keeps only the
+        # tail of a long line (the driver's record) still has config 2's latency, the frame and every leg
+        line["summary"] = summary(line, value)
         print(json.dumps(line), flush=True)
     solver.close()
     if world > 1:

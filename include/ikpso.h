@@ -144,9 +144,13 @@ ikpso_status ikpso_init_generators_seeded(ikpso_rng_state* randoms, int64_t coun
  *             a particle whose node or link box intersects one (GJK) gets fitness FLT_MAX.
  * Synchronises `stream` before returning.  After the argument checks, an error the
  * caller's earlier HIP work left pending (unread by hipGetLastError) is returned
- * (IKPSO_ERR_HIP, ikpso_last_hip_error) and consumed, and nothing runs -- the reference
- * reports it the same way, from its first cudaGetLastError check
- * (src/kernel.cu:293-295); ikpso_solve_batch does the same. */
+ * (IKPSO_ERR_HIP, ikpso_last_hip_error) and consumed up front, and nothing runs:
+ * particles, bests, randoms and result are left untouched.  The reference returns
+ * such an error too (its first cudaGetLastError check, src/kernel.cu:293-295), but
+ * only after its init kernels have rewritten particles, bests and randoms.
+ * ikpso_solver_create and ikpso_solve_batch take a pending error the same way
+ * (a stale error from unrelated earlier work fails them; read it with
+ * hipGetLastError first to avoid that). */
 ikpso_status ikpso_calculate_pso(float* particles, const float* positions, float* bests,
                                  ikpso_rng_state* randoms, int size, const ikpso_node* chain, int node_count,
                                  ikpso_pso_config pso, ikpso_fitness_config fit, float* result,
@@ -265,6 +269,11 @@ ikpso_status ikpso_solver_generator_states(ikpso_solver* solver, int64_t first_s
 /* Introspection.  dof = D, the free dimensions. */
 int ikpso_solver_dof(const ikpso_solver* solver);
 int ikpso_solver_effectors(const ikpso_solver* solver);
+/* Colliders the solver's kernels test: the descriptor's collider_count, or 0 when
+ * none lies within the arm's reach of any node (the term can then never
+ * contribute, and the chain is solved by the kernels without it; the environment
+ * variable IKPSO_KEEP_FAR_COLLIDERS=1 keeps it). */
+int ikpso_solver_collider_count(const ikpso_solver* solver);
 /* Name of the kernel variant the solver dispatches to (family / topology); after a
  * solve_batch that AUTO routed to the cooperative latency variant (a few swarms),
  * that variant's name until the next solve. */

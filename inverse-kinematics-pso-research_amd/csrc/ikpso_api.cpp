@@ -168,11 +168,14 @@ ikpso_status fetch_any(void* dst, const void* src, size_t bytes)
 }
 
 // An error the caller's earlier HIP work left pending (not yet read by
-// hipGetLastError) is reported by the next solver call, which then does nothing:
-// the reference's calculatePSO returns it the same way, from its first
-// cudaGetLastError check (src/kernel.cu:293-295).  Taking it here also keeps it from
-// being mistaken for a launch failure of this call (the launches are checked with
-// hipGetLastError).
+// hipGetLastError) is reported up front by the next entry point that runs HIP
+// work (calculate_pso, solver_create, solve_batch), which then leaves every buffer
+// and the solver state untouched.  The reference's calculatePSO also returns such
+// an error, from its first cudaGetLastError check (src/kernel.cu:293-295), but only
+// after its init kernels have already rewritten particles, bests and randoms.
+// Taking it here also keeps it from being mistaken for a launch failure of this
+// call (the launches are checked with hipGetLastError) and from being cleared by
+// fetch_any / is_device_memory, which clear the errors their own lookups cause.
 hipError_t take_pending_error() { return hipGetLastError(); }
 
 struct Extras {
@@ -374,6 +377,33 @@ ikpso_status parse_chain(const std::vector<ikpso_node>& nodes, const ikpso_pso_c
             if (!std::isfinite(lim)) return IKPSO_ERR_INVALID_ARG;
             ch.aux[ch.coll_lim_off + (size_t)(k - 1) * ch.num_coll + i] = (float)(lim * lim);
         }
+    }
+    // Host-side early-out: every node (and link midpoint) lies within the arm's length
+    // sum_k |len_k| of the origin's position, so a collider farther from it than that
+    // plus near_collider's limit for every node can never pass the inline sphere test,
+    // let alone GJK (the margin covers the fp32 FK's rounding, ~1e-6 of the reach).
+    // When that holds for every collider the term contributes nothing to any fitness:
+    // the chain is solved without it, by the plain kernels -- bit-identical answers in
+    // REFERENCE arithmetic (the same reference operation order), and in FAST the
+    // plain kernels' own arithmetic.  IKPSO_KEEP_FAR_COLLIDERS=1 keeps the term (to
+    // time the collider kernels with nothing near).
+    if (ch.num_coll > 0) {
+        double arm = 0.0;
+        for (int k = 1; k <= J; ++k) arm += fabs((double)ch.len[k]);
+        bool reachable = false;
+        for (int i = 0; i < ch.num_coll && !reachable; ++i) {
+            const CollRec r = collider_record(ex.colliders[i]);
+            const double dx = (double)r.px - ch.m0[3], dy = (double)r.py - ch.m0[7], dz = (double)r.pz - ch.m0[11];
+            const double dist = sqrt(dx * dx + dy * dy + dz * dz);
+            const double margin = 1e-3 + 1e-4 * (arm + dist + fabs((double)r.px) + fabs((double)r.py) + fabs((double)r.pz));
+            for (int k = 1; k <= J && !reachable; ++k) {
+                const double lim = sqrt((double)ch.aux[ch.coll_lim_off + (size_t)(k - 1) * ch.num_coll + i]);
+                reachable = dist - arm <= lim + margin;
+            }
+        }
+        const char* keep = getenv("IKPSO_KEEP_FAR_COLLIDERS");
+        ch.colliders_far = !reachable;
+        if (!reachable && !(keep && keep[0] == '1')) ch.num_coll = 0;
     }
     if (ch.use_posref && ex.positions)
         for (int i = 0; i < 4 * J; ++i) ch.aux[i] = ex.positions[i + (ex.posref_node_slot ? 8 : 0)];
@@ -1010,6 +1040,9 @@ ikpso_status ikpso_solver_create(const ikpso_solver_desc* desc, ikpso_solver** o
         return IKPSO_ERR_INVALID_ARG;
     if (desc->arith != IKPSO_ARITH_FAST && desc->arith != IKPSO_ARITH_REFERENCE) return IKPSO_ERR_INVALID_ARG;
     *out = nullptr;
+    // a caller's pending error is reported here, before fetch_any's own lookups
+    // (which clear the errors they cause) could discard it
+    IKPSO_HIP(take_pending_error());
     const int J = desc->node_count - 1;
     std::vector<ikpso_node> nodes(desc->node_count);
     ikpso_status st = fetch_any(nodes.data(), desc->chain, sizeof(ikpso_node) * desc->node_count);
@@ -1321,6 +1354,7 @@ ikpso_status ikpso_solver_evaluate(ikpso_solver* s, const float* angles, const f
 
 int ikpso_solver_dof(const ikpso_solver* s) { return s ? s->chain.dof() : 0; }
 int ikpso_solver_effectors(const ikpso_solver* s) { return s ? s->chain.E : 0; }
+int ikpso_solver_collider_count(const ikpso_solver* s) { return s ? s->chain.num_coll : 0; }
 const char* ikpso_solver_kernel_name(const ikpso_solver* s)
 {
     return s ? (s->last_latency ? s->kname_latency : s->kname).c_str() : "";

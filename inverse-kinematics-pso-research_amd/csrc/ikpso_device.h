@@ -133,8 +133,8 @@ __host__ __device__ inline void xorwow_seed(uint64_t seed, uint32_t st[6])
 // |x| < 2^12), minimax polynomials on [-pi/4, pi/4] (sin odd degree 7, cos
 // Horner in z = r^2), quadrant fix-up by one select pair and two bitop3 sign
 // flips.  Measured on gfx950 against correctly rounded sin/cos over 2^26
-// arguments in [-100, 100]: max 1 ulp, 71-73% correctly rounded
-// (tools/probes/trig_probe.hip).
+// arguments in [-100, 100]: 71-73% correctly rounded (tools/probes/trig_probe.hip);
+// exhaustively over every float |x| < 4096: max 2 ulp, 7.2e-8 abs.
 // TRIG 1 (kTrigHw): the transcendental unit instead (below); TRIG 2 (kTrigHwRev):
 // the same with the angle given in revolutions (kTermRev kernels), so the
 // conversion multiply disappears.
@@ -578,8 +578,12 @@ using RngFor = XorwowT<!(TERMS & kTermColliders)>;
 // FAST sin/cos on the transcendental unit (sincos_fast<true>) for a kernel of
 // this topology and term set: chains that run 4 waves per SIMD, no collider term
 // (whose contact decisions the tests compare across kernels bit for bit).
+#ifndef IKPSO_COLLIDE_HW_TRIG
+#define IKPSO_COLLIDE_HW_TRIG 0  // experiment: the unmasked collider builds on the transcendental unit too
+#endif
 template <class Topo, int MODE, int TERMS>
-constexpr bool kHwTrigOk = IKPSO_FAST_HW_TRIG && MODE == IKPSO_ARITH_FAST && !(TERMS & kTermColliders) && Topo::D <= 60;
+constexpr bool kHwTrigOk = IKPSO_FAST_HW_TRIG && MODE == IKPSO_ARITH_FAST && Topo::D <= 60 &&
+                           (!(TERMS & kTermColliders) || (IKPSO_COLLIDE_HW_TRIG && !(TERMS & kTermMask)));
 // The sin/cos flavour of a kernel build (sincos_fast): polynomial, hardware on
 // radians, or hardware on revolutions (kTermRev).
 template <class Topo, int MODE, int TERMS>
@@ -587,6 +591,14 @@ constexpr int kHwTrig = !kHwTrigOk<Topo, MODE, TERMS> ? ((TERMS & kTermRev) ? kT
                        : (TERMS & kTermRev) ? kTrigHwRev : kTrigHw;
 template <class Topo, int MODE, int TERMS>
 constexpr bool kRev = (TERMS & kTermRev) != 0;
+// Link k's length for a build whose sin/cos flavour is HW: the transcendental
+// unit's builds read the lengths compensated for its amplitude bias
+// (ChainConsts::len_hw, kHwTrigAmplitudeBias), every other build the chain's own.
+template <int HW, class CC>
+__device__ __forceinline__ float link_len(const CC& cc, int k)
+{
+    return (HW == kTrigHw || HW == kTrigHwRev) ? cc.len_hw[k] : cc.len[k];
+}
 // angle / penalty weights of a build (kTermRev: the (2 pi)^2 of the revolution units)
 template <int TERMS, class CC>
 __device__ __forceinline__ float angle_weight(const CC& cc) { return (TERMS & kTermRev) ? cc.aw_rev : cc.aw_j; }
@@ -669,11 +681,11 @@ struct FitnessAcc {
             sincos_fast<HW>(a, &sa, &ca);
             sincos_fast<HW>(b, &sb, &cb);
             sincos_fast<HW>(c, &sc, &cc_);
-            F[k] = root_frame_sc(sa, ca, sb, cb, sc, cc_, cc.len[k]);
+            F[k] = root_frame_sc(sa, ca, sb, cb, sc, cc_, link_len<HW>(cc, k));
         } else if (seq(k)) {
-            F[k] = child_frame<MODE, true, HW>(F[pk], a, b, c, cc.len[k]);
+            F[k] = child_frame<MODE, true, HW>(F[pk], a, b, c, link_len<HW>(cc, k));
         } else {
-            F[k] = child_frame<MODE, false, HW>(F[pk], a, b, c, cc.len[k]);
+            F[k] = child_frame<MODE, false, HW>(F[pk], a, b, c, link_len<HW>(cc, k));
         }
         terms(cc, k, a, b, c, rest3, tgt3, node_pos);
     }
@@ -684,12 +696,14 @@ struct FitnessAcc {
     {
         static_assert(MODE == IKPSO_ARITH_FAST, "precomputed sin/cos: FAST arithmetic");
         const int pk = Topo::kGeneric ? cc.parent[k] : Topo::parent(k);
+        constexpr int HW = kHwTrig<Topo, MODE, TERMS>;
+        const float len = link_len<HW>(cc, k);
         if (kOriginFrame<Topo, TERMS> && pk == 0)
-            F[k] = root_frame_sc(t.s[0], t.c[0], t.s[1], t.c[1], t.s[2], t.c[2], cc.len[k]);
+            F[k] = root_frame_sc(t.s[0], t.c[0], t.s[1], t.c[1], t.s[2], t.c[2], len);
         else if (seq(k))
-            F[k] = child_frame_fast_seq_sc(F[pk], t.s[0], t.c[0], t.s[1], t.c[1], t.s[2], t.c[2], cc.len[k]);
+            F[k] = child_frame_fast_seq_sc(F[pk], t.s[0], t.c[0], t.s[1], t.c[1], t.s[2], t.c[2], len);
         else
-            F[k] = child_frame_fast_sc(F[pk], t.s[0], t.c[0], t.s[1], t.c[1], t.s[2], t.c[2], cc.len[k]);
+            F[k] = child_frame_fast_sc(F[pk], t.s[0], t.c[0], t.s[1], t.c[1], t.s[2], t.c[2], len);
         terms(cc, k, ang[0], ang[1], ang[2], rest3, tgt3, node_pos);
     }
 
@@ -991,7 +1005,7 @@ struct TipBackAcc {
     __device__ __forceinline__ void back(const ChainConsts<J>& cc, int k, const NodeTrig<3>& t)
     {
         const float sa = t.s[0], ca = t.c[0], sb = t.s[1], cb = t.c[1], sc = t.s[2], cc_ = t.c[2];
-        const float l = cc.len[k];
+        const float l = link_len<HW>(cc, k);
         float w0, w1, w2;
         if (k == J) {  // Rz (l, 0, 0)
             w0 = cc_ * l;
@@ -1149,10 +1163,10 @@ __device__ __forceinline__ float residual(const ChainConsts<Topo::J>& cc, const 
                 sincos_fast<HW>(x[3 * (k - 1)], &sa, &ca);
                 sincos_fast<HW>(x[3 * (k - 1) + 1], &sb, &cb);
                 sincos_fast<HW>(x[3 * (k - 1) + 2], &sc, &cc_);
-                F[k] = root_frame_sc(sa, ca, sb, cb, sc, cc_, cc.len[k]);
+                F[k] = root_frame_sc(sa, ca, sb, cb, sc, cc_, link_len<HW>(cc, k));
             } else {
                 F[k] = child_frame<MODE, false, HW>(F[pk], x[3 * (k - 1)], x[3 * (k - 1) + 1], x[3 * (k - 1) + 2],
-                                                    cc.len[k]);
+                                                    link_len<HW>(cc, k));
             }
             if (Topo::effector(k) && cc.eff_slot[k] >= 0) {
                 const float dx = tgt[3 * (k - 1) + 0] - F[k].px;

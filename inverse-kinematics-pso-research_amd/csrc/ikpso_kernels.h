@@ -68,7 +68,8 @@ struct ChainHost {
     bool unit_rev_bounds = false; // ... and they are [0, 1] in revolutions (kTermUnitBounds): [0, 2pi]
     bool ordered_bounds = false;  // ... and finite with lo <= hi (REFERENCE uniform builds: median clamp)
     bool sym_penalty = false;     // soft limits symmetric and within a revolution of the clamp (kTermSymPenalty)
-    int num_coll = 0;             // colliders (obj_t) of the scene
+    int num_coll = 0;             // colliders (obj_t) of the scene; 0 when none is within reach
+    bool colliders_far = false;   // the scene has colliders, none within the arm's reach (parse_chain)
     size_t coll_off = 0;          // float offset of the collider records in aux
     size_t coll_lim_off = 0;      // ... of near_collider's squared limits [J][num_coll] (after the records)
     // joint-axis mask over the kernel's dimensions (all set: no mask) and the
@@ -160,13 +161,32 @@ constexpr int kCoopLatencyThreads = 256;
 // grows with |x|).  Chains whose clamp bounds or rest angles reach beyond it
 // solve with the 1-ulp polynomial instead (ChainHost::poly_trig).
 constexpr float kHwTrigMaxAbs = 100.0f;
+// The transcendental unit's v_sin_f32 / v_cos_f32 round toward zero more often
+// than not: over a revolution e_sin = -eps sin, e_cos = -eps cos with eps =
+// 3.23e-8 (tools/probes/hwtrig_bias.hip, profiles/r05/hwtrig_bias.txt), so each
+// plane rotation built from them shrinks the in-plane part of the vector it turns
+// by eps.  A link vector passes the 3 plane rotations of every node from the root
+// to its own node (in the frame-composition and the tip-backward forms alike:
+// the rotations' product is the same); with an isotropic in-plane share of 2/3
+// that is an expected shrink of 2 depth(k) eps for link k -- 7.7e-7 of the reach
+// of config 5's 20-joint chain, a median +1.4e-6 of its final fitness (round 5's
+// strict sign test: 83 worse / 44 better than the oracle).  The FAST kernels on
+// the transcendental unit therefore use link lengths scaled up by that much
+// (ChainConsts::len_hw; fp64, rounded once): the strict count became 55 / 66
+// (profiles/r06/hwtrig_comp.txt).  Per value no fp32 correction exists (1 + eps
+// rounds back to 1); per link the scaled length is representable.
+constexpr double kHwTrigAmplitudeBias = 3.23e-8;
 template <int J>
 ChainConsts<J> make_consts(const ChainHost& h)
 {
     ChainConsts<J> c;
     memset(&c, 0, sizeof(c));
+    int depth[J + 1];
+    depth[0] = 0;
+    for (int k = 1; k <= J; ++k) depth[k] = (h.parent[k] > 0 ? depth[h.parent[k]] : 0) + 1;
     for (int k = 0; k <= J; ++k) {
         c.len[k] = h.len[k];
+        c.len_hw[k] = k ? (float)((double)h.len[k] * (1.0 + 2.0 * depth[k] * kHwTrigAmplitudeBias)) : h.len[k];
         c.eff_w[k] = h.eff_w[k];
         c.eff_slot[k] = h.eff_slot[k];
         c.parent[k] = h.parent[k];

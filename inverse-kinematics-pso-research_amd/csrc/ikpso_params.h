@@ -16,6 +16,10 @@ constexpr int kMaxJoints = 32;
 template <int J>
 struct ChainConsts {
     float len[J + 1];
+    // The link lengths the FAST kernels on the transcendental unit's sin/cos use:
+    // len[k] * (1 + 2 depth(k) eps), rounded once from fp64 (make_consts).  See
+    // kHwTrigAmplitudeBias (ikpso_kernels.h) and link_len (ikpso_device.h).
+    float len_hw[J + 1];
     float eff_w[J + 1];
     int32_t eff_slot[J + 1];  // effector ordinal among effectors, -1 otherwise
     int32_t parent[J + 1];    // used by the generic-topology kernels only

@@ -144,6 +144,7 @@ SIGNATURES = {
     "ikpso_solver_generator_states": (_i32, [_vp, _i64, _i64, _vp, _vp]),
     "ikpso_solver_dof": (ctypes.c_int, [_vp]),
     "ikpso_solver_effectors": (ctypes.c_int, [_vp]),
+    "ikpso_solver_collider_count": (ctypes.c_int, [_vp]),
     "ikpso_solver_kernel_name": (ctypes.c_char_p, [_vp]),
     "ikpso_abi_version": (ctypes.c_int, []),
     "ikpso_status_string": (ctypes.c_char_p, [_i32]),

@@ -212,6 +212,11 @@ class BatchSolver:
         self.capacity = 0
 
     @property
+    def collider_count(self) -> int:
+        """Colliders the kernels test (0 when none is within the arm's reach)."""
+        return self._lib.ikpso_solver_collider_count(self._h)
+
+    @property
     def kernel(self) -> str:
         """Kernel variant the solver dispatches to (the last solve's, once one ran)."""
         return self._lib.ikpso_solver_kernel_name(self._h).decode()

@@ -177,3 +177,116 @@ def test_resident_full_swarm_colliders_reference_bitexact(oracle, device, scene,
     oang, ofit, ores = oracle.solve_batch(wl.chain, tg, None, P, I, ostate, colliders=boxes, threads=8,
                                           axis_mask=mask)
     assert np.array_equal(ang, oang) and np.array_equal(fit, ofit)
+
+
+def test_collide_leg_tier_b(oracle, device, report):
+    """The bench's collide leg at its own configuration (bench.py collide_leg: config 3's
+    targets, 1024 particles x 500 iterations, the reference's initColliders boxes 0 and 3,
+    src/Main.cpp:537-559; the term src/kernel.cu:104-136), FAST, on the 256 swarms of
+    tests/golden/tierb_collide.npz: the stated tests of tests/tierb.py against the oracle's
+    FMA on/off envelope (Fisher tests of the shares with the absolute floor, strict sign test
+    of the fitness, alpha = 0.01), gross-error ceilings at twice the envelope's worst swarm,
+    mean fitness within 0.5 %, every answer collision-free with the device's own evaluation
+    of it equal to the reported fitness, generator states bit-exact.  This covers the
+    improving-lanes filter (ikpso_collide.h: only lanes whose collision-free value could
+    pass the strict local-best update run GJK) over whole FAST solves."""
+    from tierb import envelope, load_fixture, stat_tests, tier_b_distances, tier_b_report
+
+    wl = ikpso.workload(3)
+    fx = load_fixture("collide")
+    boxes = ikpso.init_colliders(4)[[0, 3]]
+    B, P, I, D = int(fx["swarms"]), wl.particles, wl.iterations, wl.dof
+    tg = wl.targets(0, B)
+    s = ikpso.BatchSolver(wl.chain, P, pso=wl.pso, colliders=boxes)
+    s.seed(B)
+    ang, fit, res = (t.cpu().numpy() for t in s.solve(dev(tg), iterations=I))
+    assert "resident" in s.kernel, s.kernel
+    efit = s.evaluate(dev(ang), dev(tg))[0].cpu().numpy()
+    states = s.generator_states(0, B)
+    s.close()
+    want = oracle.skipahead(oracle.init_generators(B * P, 0), D + 3 * D * I)
+    assert np.array_equal(states[:, :6], want.view(np.int32).reshape(-1, 12)[:, :6])
+    assert (fit < FMAX).all() and np.isfinite(ang).all()
+    assert np.array_equal(efit, fit)  # one arithmetic: the solve's fitness is the evaluate kernel's
+    env = envelope(wl.chain, fx)
+    rang, rfit, rres = fx["ref_angles"], fx["ref_fitness"], fx["ref_residual"]
+    dist = tier_b_distances(wl.chain, ang, fit, res, rang, rfit, rres)
+    rep = tier_b_report(*dist)
+    tests = stat_tests(dist, env, fit, rfit)
+    rep.update(mean_fitness=float(fit.mean()), oracle_mean_fitness=float(rfit.mean()), envelope=tier_b_report(*env),
+               tests=tests)
+    report("tier_b_collide", rep)
+    assert tests["pass"], tests
+    for d, e in zip(dist, env):
+        assert d.max() <= 2 * e.max(), (d.max(), e.max())
+    assert abs(fit.mean() - rfit.mean()) / rfit.mean() < 5e-3
+    assert abs(res.mean() - rres.mean()) < 1e-3 + 0.01 * rres.mean()
+    # the oracle's own verdict on the answers: clear of the boxes (within FMA rounding of the
+    # reference-order FK: against boxes shrunk by 1 %)
+    shrunk = boxes.copy()
+    for ax in ("x", "y", "z"):
+        shrunk[ax] *= 0.99
+    assert all(oracle.fitness(_with_targets(wl.chain, tg[b]), ang[b], colliders=shrunk) < FMAX for b in range(B))
+
+
+def test_collide_leg_reference_whole_solve(oracle, device):
+    """REFERENCE arithmetic over whole solves of the collide leg (500 iterations), the first
+    8 swarms of tests/golden/tierb_collide.npz: angles and fitness bit-identical to the
+    oracle's, so the improving-lanes filter changes no decision over a full solve."""
+    from tierb import load_fixture
+
+    wl = ikpso.workload(3)
+    fx = load_fixture("collide")
+    boxes = ikpso.init_colliders(4)[[0, 3]]
+    B, P, I = 8, wl.particles, wl.iterations
+    s = ikpso.BatchSolver(wl.chain, P, pso=wl.pso, arith="reference", colliders=boxes)
+    s.seed(B)
+    ang, fit, res = (t.cpu().numpy() for t in s.solve(dev(wl.targets(0, B)), iterations=I))
+    assert "resident" in s.kernel, s.kernel
+    s.close()
+    assert np.array_equal(ang, fx["ref_angles"][:B]) and np.array_equal(fit, fx["ref_fitness"][:B])
+    assert np.max(np.abs(res - fx["ref_residual"][:B])) <= 1e-5
+
+
+@pytest.mark.parametrize("arith", ["reference", "fast"])
+def test_far_colliders_skip_the_term(oracle, device, monkeypatch, arith):
+    """Host-side early-out (parse_chain): colliders beyond the arm's reach of every node
+    (the reference's four initColliders boxes moved 1000 units away) can never pass the
+    inline sphere test, so the solver drops the term and runs the plain kernels.
+    REFERENCE: bit-exact to the oracle with the colliders (its GJK runs and finds nothing)
+    and to the same solver kept on the collider kernel (IKPSO_KEEP_FAR_COLLIDERS=1).
+    FAST: bit-identical to a solver without colliders; a box within reach keeps the term."""
+    wl = ikpso.workload(3)
+    far = ikpso.init_colliders(4)
+    far["pos"] += 1000.0
+    B, P, I = 4, 1024, 12
+    tg = wl.targets(0, B)
+
+    def solve(boxes):
+        s = ikpso.BatchSolver(wl.chain, P, pso=ikpso.PSOConfig(0.5, 0.5, 1.25, I), arith=arith, colliders=boxes)
+        n = s.collider_count
+        s.seed(B)
+        out = [t.cpu().numpy() for t in s.solve(dev(tg), iterations=I)]
+        s.close()
+        return n, out
+
+    monkeypatch.delenv("IKPSO_KEEP_FAR_COLLIDERS", raising=False)
+    n_far, (ang, fit, res) = solve(far)
+    assert n_far == 0
+    n_none, (ang0, fit0, res0) = solve(None)
+    assert n_none == 0 and np.array_equal(ang, ang0) and np.array_equal(fit, fit0)
+    near = ikpso.init_colliders(4)[[0, 3]]
+    assert solve(near)[0] == 2
+    # a box just beyond the reach bound is dropped, one just inside kept
+    arm = float(np.abs(wl.chain["length"][1:]).sum())
+    edge = ikpso.make_collider((0.2, 0.2, 0.2), (arm + 2.0, 0.0, 0.0))
+    assert solve(edge)[0] == 0
+    edge["pos"][0] = (arm, 0.0, 0.0)
+    assert solve(edge)[0] == 1
+    if arith == "reference":
+        ostate = oracle.init_generators(B * P, 0)
+        oang, ofit, ores = oracle.solve_batch(wl.chain, tg, None, P, I, ostate, colliders=far, threads=8)
+        assert np.array_equal(ang, oang) and np.array_equal(fit, ofit)
+        monkeypatch.setenv("IKPSO_KEEP_FAR_COLLIDERS", "1")
+        n_keep, (angk, fitk, _) = solve(far)
+        assert n_keep == 4 and np.array_equal(angk, ang) and np.array_equal(fitk, fit)

@@ -1,0 +1,45 @@
+#!/usr/bin/env python3
+"""Diagnostic (GPU): do the FAST collider solve kernel and the FAST evaluate kernel compute
+the same fitness for the solve's answers?  test_batch_with_colliders_fast's setup (32 swarms x
+256 x 40, a box between the arm and its targets) plus the collide leg's (config 3 targets,
+boxes 0 and 3, 64 swarms x 1024 x 500).  Prints, per setup, how many reported fitness
+values differ from the evaluate kernel's of the same angles, how many of those are contact
+decisions (one side FLT_MAX), and the largest relative difference of the others."""
+import json
+import sys
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path[:0] = [str(ROOT / "inverse-kinematics-pso-research_amd")]
+import torch  # noqa: E402
+
+import ikpso  # noqa: E402
+
+FMAX = np.float32(np.finfo(np.float32).max)
+
+
+def run(name, chain, boxes, tg, P, I, pso):
+    s = ikpso.BatchSolver(chain, P, pso=pso, colliders=boxes)
+    B = len(tg)
+    s.seed(B)
+    t = torch.from_numpy(np.ascontiguousarray(tg)).cuda()
+    ang, fit, res = (x.cpu().numpy() for x in s.solve(t, iterations=I))
+    efit = s.evaluate(torch.from_numpy(ang).cuda(), t)[0].cpu().numpy()
+    kern = s.kernel
+    s.close()
+    diff = fit != efit
+    contact = diff & ((fit == FMAX) | (efit == FMAX))
+    fin = diff & ~contact
+    rel = np.abs(fit[fin] - efit[fin]) / np.abs(efit[fin]) if fin.any() else np.zeros(1)
+    print(json.dumps({"setup": name, "kernel": kern, "swarms": B, "differ": int(diff.sum()), "contact": int(contact.sum()),
+                      "max_rel_other": float(rel.max()), "reported_fmax": int((fit == FMAX).sum()),
+                      "evaluate_fmax": int((efit == FMAX).sum())}), flush=True)
+
+
+if __name__ == "__main__":
+    wl = ikpso.workload(3)
+    boxes = np.concatenate([ikpso.make_collider((0.6, 0.6, 0.6), (0.0, 0.9, -1.6)), ikpso.init_colliders(1)])
+    run("test_batch_with_colliders_fast", wl.chain, boxes, wl.targets(0, 32), 256, 40, ikpso.PSOConfig(0.5, 0.5, 1.25, 40))
+    run("collide_leg_64", wl.chain, ikpso.init_colliders(4)[[0, 3]], wl.targets(0, 64), 1024, 500, wl.pso)

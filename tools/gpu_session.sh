@@ -9,11 +9,16 @@
 #   bench        the default bench line (BENCH_ARGS adds flags) -> gpurun_out/bench.json
 #   bench:<cfg>  bench.py --config <cfg> (3 steps) -> gpurun_out/bench_<cfg>.json
 #   gloo2        the N = 2 path rehearsed on the one GPU (two ranks over gloo sharing it; not a
-#                measurement): the default line with its config-4 leg at 2 x 8192 targets
+#                measurement): the default line with its config-4 leg at 2 x 8192 targets and
+#                rank 0's CPU baseline
 #   rocprof      rocprofv3 kernel trace of the default bench command (its average kernel
 #                duration must agree with the line's HIP-event kernel_ms)
 #   profile:<n>  kernel trace + PMC passes (tools/gpu_profile.sh) of workload n in
 #                {c3, c5, dh7, c3ref, collide}: the counters bench.py's roofline reads
+#   hwcomp       v_sin/v_cos amplitude error on the tier-B answers' angles + the link-length
+#                compensation experiment (tools/hwtrig_comp.py; HWCOMP_EPS = eps list)
+#   collconsist  FAST collider solve vs evaluate kernel (tools/collide_consistency.py; VLIBS = variants)
+#   collcmp      collider kernel ms, boxes near / far (tools/collide_cmp.sh; VARIANTS = product coll_vN ...)
 #   frame        the visualiser frame latency (tools/frame_bench.py)
 #   collstats    collider-term counters (tools/collide_stats.py) with vlib/collide_stats.so
 #   frametrace   rocprofv3 kernel trace of the same (what device work one frame issues)
@@ -44,7 +49,7 @@ for s in "$@"; do
       step "bench_$c" 600 python bench.py --config "$c" --steps 3 --warmup 1 --cpu-seconds 4 || exit 4
       tail -1 "gpurun_out/bench_$c.log" > "gpurun_out/bench_$c.json" ;;
     gloo2)
-      step gloo2 600 python bench.py --gpus 2 --dist-backend gloo --steps 3 --warmup 1 --cpu-seconds 0 || exit 4
+      step gloo2 600 python bench.py --gpus 2 --dist-backend gloo --steps 3 --warmup 1 --cpu-seconds 4 || exit 4
       grep '^{' gpurun_out/gloo2.log | tail -1 > gpurun_out/bench_gloo2.json ;;
     rocprof)
       step rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_default -o run --output-format csv -- \
@@ -59,6 +64,17 @@ for s in "$@"; do
                      --cpu-seconds 0" bash tools/gpu_profile.sh || exit 6 ;;
     profile:c5) PROF_NAME=c5 PROF_ARGS="--config 5 --swarms-per-gpu 2048 --iterations 100 --steps 1 --warmup 1 \
                 --cpu-seconds 0" bash tools/gpu_profile.sh || exit 6 ;;
+    hwcomp)  # the transcendental unit's amplitude error on the fixtures' answer angles, and the link-length
+             # compensation experiment (tools/hwtrig_comp.py)
+      python -c "import numpy as np; [np.load(f'tests/golden/tierb_config{c}.npz')['ref_angles'].astype(np.float32).tofile(f'gpurun_out/c{c}_angles.f32') for c in (3, 5)]" || exit 11
+      step hwprobe 120 tools/probes/hwtrig_bias gpurun_out/c5_angles.f32 gpurun_out/c3_angles.f32 || exit 11
+      step hwcomp 600 python -u tools/hwtrig_comp.py ${HWCOMP_EPS:-} || exit 11 ;;
+    collconsist)  # FAST collider solve vs evaluate kernel on the solve's answers (product, then VLIBS variants)
+      step collconsist_product 300 python -u tools/collide_consistency.py || exit 12
+      for v in ${VLIBS:-}; do
+        IKPSO_LIB=vlib/$v.so IKPSO_ALLOW_STALE=1 step "collconsist_$v" 300 python -u tools/collide_consistency.py || exit 12
+      done ;;
+    collcmp) step collcmp 900 env VARIANTS="${VARIANTS:-product}" bash tools/collide_cmp.sh || exit 13 ;;
     frame) step frame 300 python tools/frame_bench.py || exit 7 ;;
     collstats) [ -f vlib/collide_stats.so ] || { echo "no vlib/collide_stats.so"; exit 10; }
       for sc in init03 far4 init4; do

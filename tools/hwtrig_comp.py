@@ -1,0 +1,73 @@
+#!/usr/bin/env python3
+"""Experiment (GPU): does pre-scaling the link lengths undo the transcendental
+unit's amplitude bias?  v_sin_f32 / v_cos_f32 return sin/cos about eps = 3.2e-8
+too small in relative terms (profiles/r05/hwtrig_bias.txt), so every plane
+rotation of the FAST FK shrinks the in-plane part of the vector it turns by eps.
+Link k's vector passes the 3*depth(k) plane rotations of the nodes from the root
+to k; with an isotropic in-plane share of 2/3 that is an expected shrink of
+2*depth(k)*eps, undone by l_k * (1 + 2 depth(k) eps) (fp64, rounded once).
+
+Here the scaled lengths are passed in the chain table itself (no rebuild), the
+FAST answers of the tier-B fixtures' swarms are solved for each eps, and the
+stated tests of tests/tierb.py are run on the GPU's reported fitness and on the
+oracle's fitness of the GPU's angles under the unscaled chain.  Test
+infrastructure: imports oracle/ as the checker.
+usage: hwtrig_comp.py [eps ...]  -> JSON lines"""
+import json
+import sys
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path[:0] = [str(ROOT / "inverse-kinematics-pso-research_amd"), str(ROOT / "oracle"), str(ROOT / "tests")]
+import torch  # noqa: E402
+
+import ikpso  # noqa: E402
+import oracle  # noqa: E402
+from tierb import envelope, load_fixture, stat_tests, tier_b_distances  # noqa: E402
+
+
+def depths(chain):
+    d = np.zeros(len(chain), dtype=np.int64)
+    for k in range(1, len(chain)):
+        p = int(chain["parent_index"][k])
+        d[k] = (d[p] + 1) if p > 0 else 1
+    return d
+
+
+def run(cfg, eps):
+    wl = ikpso.workload(cfg)
+    fx = load_fixture(cfg)
+    B, I = int(fx["swarms"]), wl.iterations
+    ch = wl.chain.copy()
+    ch["length"] = (ch["length"].astype(np.float64) * (1.0 + 2.0 * depths(ch) * eps)).astype(np.float32)
+    s = ikpso.BatchSolver(ch, wl.particles, pso=ikpso.PSOConfig(0.5, 0.5, 1.25, I), limit_weight=wl.limit_weight,
+                          soft_lo=wl.soft_lo, soft_hi=wl.soft_hi)
+    s.seed(B)
+    tg = wl.targets(0, B)
+    ang, fit, res = (t.cpu().numpy() for t in s.solve(torch.from_numpy(tg).cuda(), iterations=I))
+    kern = s.kernel
+    s.close()
+    eff = np.flatnonzero(wl.chain["node_type"] == ikpso.NODE_EFFECTOR)
+    ofit = np.empty(B, np.float32)
+    for b in range(B):
+        c = wl.chain.copy()
+        c["target_position"][eff] = tg[b]
+        ofit[b] = oracle.fitness(c, ang[b], limit_weight=wl.limit_weight, soft_lo=wl.soft_lo, soft_hi=wl.soft_hi)
+    env = envelope(wl.chain, fx)
+    rfit = fx["ref_fitness"]
+    out = {"config": cfg, "eps": eps, "kernel": kern, "swarms": B}
+    for name, f in (("reported", fit), ("oracle_of_angles", ofit)):
+        t = stat_tests(tier_b_distances(wl.chain, ang, f, res, fx["ref_angles"], rfit, fx["ref_residual"]), env, f,
+                       rfit)
+        out[name] = {"pass": t["pass"], "sign": t["fitness_sign"],
+                     "within": [t[k]["gpu_within"] for k in ("rel_fitness", "residual_abs", "effector_pos_abs")]}
+    return out
+
+
+if __name__ == "__main__":
+    eps_list = [float(a) for a in sys.argv[1:]] or [0.0, 2.7e-8, 3.23e-8]
+    for cfg in (5, 3):
+        for eps in eps_list:
+            print(json.dumps(run(cfg, eps)), flush=True)

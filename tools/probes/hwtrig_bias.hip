@@ -59,8 +59,37 @@ static void run(const char* name, std::vector<float> x)
     report(name, x, s, c);
 }
 
-int main()
+// mean relative amplitude error sqrt(s^2 + c^2) - 1 over the angles (radians,
+// float32) of a file, as the FAST kernels evaluate them: x * (1 / 2pi) in fp32
+static void run_file(const char* path)
 {
+    FILE* f = fopen(path, "rb");
+    if (!f) return;
+    std::vector<float> x;
+    float v;
+    while (fread(&v, 4, 1, f) == 1) x.push_back(v * 0.159154943091895336f);
+    fclose(f);
+    const int n = (int)x.size();
+    float *dx, *ds, *dc;
+    hipMalloc(&dx, n * 4);
+    hipMalloc(&ds, n * 4);
+    hipMalloc(&dc, n * 4);
+    hipMemcpy(dx, x.data(), n * 4, hipMemcpyHostToDevice);
+    hipLaunchKernelGGL(k_hw, dim3((n + 255) / 256), dim3(256), 0, 0, dx, ds, dc, n);
+    std::vector<float> s(n), c(n);
+    hipMemcpy(s.data(), ds, n * 4, hipMemcpyDeviceToHost);
+    hipMemcpy(c.data(), dc, n * 4, hipMemcpyDeviceToHost);
+    hipFree(dx), hipFree(ds), hipFree(dc);
+    double amp = 0;
+    for (int i = 0; i < n; ++i) amp += sqrt((double)s[i] * s[i] + (double)c[i] * c[i]) - 1.0;
+    printf("%s: n=%d  mean amplitude error %.3e\n", path, n, amp / n);
+    report(path, x, s, c);
+}
+
+int main(int argc, char** argv)
+{
+    for (int i = 1; i < argc; ++i) run_file(argv[i]);
+    if (argc > 1) return 0;
     const int N = 1 << 24;
     std::vector<float> x(N + 1);
     for (int i = 0; i <= N; ++i) x[i] = (float)(-0.5 + (double)i / N);
