@@ -380,7 +380,14 @@ def collide_leg(ctx, steps, warmup, lib_id, plain_ms):
     far["pos"] += 1000.0
     P, I, Bl = wl.particles, wl.iterations, wl.swarms
     r = timed_leg(ctx, wl, Bl, P, I, steps, warmup, colliders=boxes)
+    # boxes out of reach: the host-side early-out drops the term (the plain kernel runs); kept on the
+    # collider kernel with IKPSO_KEEP_FAR_COLLIDERS=1 (the term's cost without any GJK)
     rf = timed_leg(ctx, wl, Bl, P, I, 1, 1, colliders=far)
+    os.environ["IKPSO_KEEP_FAR_COLLIDERS"] = "1"
+    try:
+        rk = timed_leg(ctx, wl, Bl, P, I, 1, 1, colliders=far)
+    finally:
+        os.environ.pop("IKPSO_KEEP_FAR_COLLIDERS", None)
     vpu, valu = valu_roofline(r["solver"].kernel + " [colliders]", Bl * P * I, r["kern_ms"], lib_id)
     hbm = None
     if vpu:  # the counter-measured HBM bytes per update: the near nodes' stored frames and node_collides' spills
@@ -396,15 +403,17 @@ def collide_leg(ctx, steps, warmup, lib_id, plain_ms):
            "solves_per_s": r["total"] * steps / r["elapsed"], "ms_per_step": 1e3 * r["elapsed"] / steps,
            "kernel_ms": round(r["kern_ms"], 3), "steps": steps, "warmup": warmup, "swarms_per_gpu": Bl,
            "total_swarms": r["total"], "dof": r["D"], "kernel": r["solver"].kernel,
-           "kernel_ms_far_colliders": round(rf["kern_ms"], 3), "kernel_ms_no_colliders": round(plain_ms, 3),
+           "kernel_ms_far_colliders": round(rf["kern_ms"], 3), "far_colliders_kernel": rf["solver"].kernel,
+           "far_colliders_tested": rf["solver"].collider_count,
+           "kernel_ms_far_colliders_kept": round(rk["kern_ms"], 3), "kernel_ms_no_colliders": round(plain_ms, 3),
            "roofline_frac": valu["frac"] if valu else None,
            "roofline_stale": valu["stale"] if valu else None,
            "roofline_hbm": hbm,
            "early_out": json.loads(st.read_text()) if st.exists() else None,
            "check": {"finite": r["finite"], "mean_fitness": r["mean_fitness"],
                      "mean_residual": r["mean_residual"]}}
-    r["solver"].close()
-    rf["solver"].close()
+    for x in (r, rf, rk):
+        x["solver"].close()
     return leg
 
 
@@ -452,7 +461,7 @@ def summary(line: dict, value: float) -> dict:
                                   "roofline_frac": ra["roofline_frac"]}
     for name, leg in (line.get("legs") or {}).items():
         out[name] = {"value": r3(leg["value"]), "kernel_ms": leg["kernel_ms"], "roofline_frac": leg["roofline_frac"]}
-        for k in ("kernel_ms_far_colliders", "kernel_ms_no_colliders"):
+        for k in ("kernel_ms_far_colliders", "kernel_ms_far_colliders_kept", "kernel_ms_no_colliders"):
             if k in leg:
                 out[name][k] = leg[k]
     cpu = line.get("cpu_baseline")

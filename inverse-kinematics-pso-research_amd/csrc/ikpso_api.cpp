@@ -1294,13 +1294,15 @@ ikpso_status ikpso_solver_sync(ikpso_solver* s)
     if (s->pending_timing) {  // measurement build: mean cycles per iteration over the workgroups
         std::vector<unsigned long long> t((size_t)s->pending_timing_n * 8);
         IKPSO_HIP(hipMemcpy(t.data(), s->pending_timing, t.size() * 8, hipMemcpyDeviceToHost));
-        double a = 0, b = 0, c = 0, it = 0, imp = 0, rem = 0, pol = 0;
+        double a = 0, b = 0, c = 0, it = 0, imp = 0, rem = 0, pol = 0, ah = 0;
         for (size_t i = 0; i < t.size(); i += 8)
-            a += t[i], b += t[i + 1], it += t[i + 2], c += t[i + 3], imp += t[i + 4], rem += t[i + 5], pol += t[i + 6];
+            a += t[i], b += t[i + 1], it += t[i + 2], c += t[i + 3], imp += t[i + 4], rem += t[i + 5],
+                pol += t[i + 6], ah += t[i + 7];
         fprintf(stderr,
                 "ikpso coop timing: %d workgroups, per iteration (wave 0): step %.0f, argmin barrier %.0f, "
-                "hand-off %.0f cycles; improving exchanges %.3f (won by another chunk %.3f), key polls %.2f\n",
-                s->pending_timing_n, a / it, c / it, b / it, imp / it, rem / it, pol / it);
+                "hand-off %.0f cycles (of which publish + draws ahead %.0f); improving exchanges %.3f (won by "
+                "another chunk %.3f), key polls %.2f\n",
+                s->pending_timing_n, a / it, c / it, b / it, ah / it, imp / it, rem / it, pol / it);
     }
 #endif
     if (!err) {

@@ -78,6 +78,7 @@ struct CoopShared {
     granule_t* slots;   // the group's [2][G] published records (kCoopSlot granules each)
 #if IKPSO_COOP_TIMING
     unsigned long long t_mid;  // wave 0 past the local argmin (timing builds)
+    unsigned long long t_ahead_sum;  // wave 0's publish + draws ahead, summed over the exchanges
     unsigned int n_imp, n_remote, n_polls;  // improving exchanges, ... won by another chunk, key polls
 #endif
 };
@@ -138,6 +139,9 @@ __device__ __forceinline__ void coop_exchange(SwarmShared<Topo>& sh, CoopShared<
         granule_t kraw = kPollFirst ? ld_granule(base + (size_t)(lane < G ? lane : 0) * SLOT) : tag;
         if (lane <= D) st_granule(base + (size_t)member * SLOT + lane, tag | (lane == 0 ? lmin : __float_as_uint(mine_d)));
         if (do_ahead) ahead();
+#if IKPSO_COOP_TIMING
+        cs.t_ahead_sum += __builtin_amdgcn_s_memtime() - cs.t_mid;
+#endif
         // the G key granules, in chunk order (lanes 0..G-1; G <= 64)
         uint32_t n = 0;
         int timed_out = 0;
@@ -261,6 +265,7 @@ __global__ void __launch_bounds__(BLOCK, (kCoopBoundWaves<Topo::D, BLOCK, TERMS>
         cs.b = group;
 #if IKPSO_COOP_TIMING
         cs.n_imp = cs.n_remote = cs.n_polls = 0;
+        cs.t_ahead_sum = 0;
 #endif
         cs.slots = io.coop_slots + (size_t)group * 2 * G * kCoopSlot(D);
     }
@@ -342,7 +347,9 @@ __global__ void __launch_bounds__(BLOCK, (kCoopBoundWaves<Topo::D, BLOCK, TERMS>
             tm[4] += cs.n_imp;
             tm[5] += cs.n_remote;
             tm[6] += cs.n_polls;
+            tm[7] += cs.t_ahead_sum;
             cs.n_imp = cs.n_remote = cs.n_polls = 0;
+            cs.t_ahead_sum = 0;
         }
 #endif
 
@@ -578,6 +585,7 @@ __global__ void __launch_bounds__(2 * kCoopLatencyThreads) k_swarm_coop_split(co
         cs.b = group;
 #if IKPSO_COOP_TIMING
         cs.n_imp = cs.n_remote = cs.n_polls = 0;
+        cs.t_ahead_sum = 0;
 #endif
         cs.slots = io.coop_slots + (size_t)group * 2 * G * kCoopSlot(D);
     }
@@ -660,7 +668,9 @@ __global__ void __launch_bounds__(2 * kCoopLatencyThreads) k_swarm_coop_split(co
             tm[4] += cs.n_imp;
             tm[5] += cs.n_remote;
             tm[6] += cs.n_polls;
+            tm[7] += cs.t_ahead_sum;
             cs.n_imp = cs.n_remote = cs.n_polls = 0;
+            cs.t_ahead_sum = 0;
         }
 #endif
 

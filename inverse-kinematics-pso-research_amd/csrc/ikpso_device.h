@@ -158,7 +158,12 @@ __host__ __device__ __forceinline__ void sincos_fast(float x, float* s_out, floa
         // 3 instructions per angle against ~20 for the polynomial: -7 % kernel
         // time on the reference scene, -9 % on the 2-wave D = 60 cooperative
         // kernel once its loop stopped spilling (it was +13 % before).
-        const float rev = x * 0.159154943091895336f;
+        // x / 2pi with the constant in two parts: fl(1 / 2pi) = 0.15915494f is 4.0e-8
+        // (relative) short of 1 / 2pi, so x * 0.15915494f turns every joint by that
+        // fraction less than x -- a bias the optimiser answers with larger angles, which
+        // the angle term then prices (round 6: the collider builds' strict tier-B count
+        // 133 worse / 91 better).  The low part's FMA rounds the product once, unbiased.
+        const float rev = __builtin_fmaf(x, 6.42063833e-9f, x * 0.159154936671257019f);
         *s_out = __builtin_amdgcn_sinf(rev);
         *c_out = __builtin_amdgcn_cosf(rev);
         return;
@@ -498,6 +503,60 @@ __device__ __forceinline__ Frame root_frame_sc(float sa, float ca, float sb, flo
     return W;
 }
 
+// FAST with every rounding pinned (the collider builds): the same column rotations
+// as child_frame_fast_seq_sc and the same closed form as root_frame_sc, with each
+// multiply-add written as the fma it is and contraction off, so every kernel that
+// evaluates a frame -- the solve's step, its initial fitness, the evaluate kernel --
+// computes it bit for bit alike, whatever the compiler would fuse in its context.
+// The collider term makes a discrete decision on the frames (GJK), and PSO drives
+// answers onto an obstacle's surface, where one ulp decides contact.
+__device__ __forceinline__ Frame child_frame_pinned_sc(const Frame& P, float sa, float ca, float sb, float cb,
+                                                       float sc, float cc, float len)
+{
+#pragma clang fp contract(off)
+    const float x01 = __builtin_fmaf(P.r02, sa, P.r01 * ca), x02 = __builtin_fmaf(-P.r01, sa, P.r02 * ca);
+    const float x11 = __builtin_fmaf(P.r12, sa, P.r11 * ca), x12 = __builtin_fmaf(-P.r11, sa, P.r12 * ca);
+    const float x21 = __builtin_fmaf(P.r22, sa, P.r21 * ca), x22 = __builtin_fmaf(-P.r21, sa, P.r22 * ca);
+    const float y00 = __builtin_fmaf(-x02, sb, P.r00 * cb), y02 = __builtin_fmaf(x02, cb, P.r00 * sb);
+    const float y10 = __builtin_fmaf(-x12, sb, P.r10 * cb), y12 = __builtin_fmaf(x12, cb, P.r10 * sb);
+    const float y20 = __builtin_fmaf(-x22, sb, P.r20 * cb), y22 = __builtin_fmaf(x22, cb, P.r20 * sb);
+    Frame W;
+    W.r00 = __builtin_fmaf(x01, sc, y00 * cc);
+    W.r01 = __builtin_fmaf(-y00, sc, x01 * cc);
+    W.r02 = y02;
+    W.r10 = __builtin_fmaf(x11, sc, y10 * cc);
+    W.r11 = __builtin_fmaf(-y10, sc, x11 * cc);
+    W.r12 = y12;
+    W.r20 = __builtin_fmaf(x21, sc, y20 * cc);
+    W.r21 = __builtin_fmaf(-y20, sc, x21 * cc);
+    W.r22 = y22;
+    W.px = __builtin_fmaf(len, W.r00, P.px);
+    W.py = __builtin_fmaf(len, W.r10, P.py);
+    W.pz = __builtin_fmaf(len, W.r20, P.pz);
+    return W;
+}
+
+__device__ __forceinline__ Frame root_frame_pinned_sc(float sa, float ca, float sb, float cb, float sc, float cc,
+                                                      float len)
+{
+#pragma clang fp contract(off)
+    const float p = sa * sb, q = ca * sb;
+    Frame W;
+    W.r00 = cb * cc;
+    W.r01 = -(cb * sc);
+    W.r02 = sb;
+    W.r10 = __builtin_fmaf(ca, sc, p * cc);
+    W.r11 = __builtin_fmaf(-p, sc, ca * cc);
+    W.r12 = -(sa * cb);
+    W.r20 = __builtin_fmaf(-q, cc, sa * sc);
+    W.r21 = __builtin_fmaf(sa, cc, q * sc);
+    W.r22 = ca * cb;
+    W.px = len * W.r00;
+    W.py = len * W.r10;
+    W.pz = len * W.r20;
+    return W;
+}
+
 // SEQ: FAST mode may compose the rotation column-wise (interior nodes, or any
 // node whose full frame is consumed).  HW: FAST sin/cos on the transcendental unit.
 template <int MODE, bool SEQ = false, int HW = kTrigPoly>
@@ -576,14 +635,24 @@ template <int TERMS>
 using RngFor = XorwowT<!(TERMS & kTermColliders)>;
 
 // FAST sin/cos on the transcendental unit (sincos_fast<true>) for a kernel of
-// this topology and term set: chains that run 4 waves per SIMD, no collider term
-// (whose contact decisions the tests compare across kernels bit for bit).
+// this topology and term set (D <= 60); of the collider builds the unmasked ones
+// of the compiled topologies (IKPSO_COLLIDE_HW_TRIG; the generic trees' collider
+// builds trip a hipcc 7.2 backend error with it -- "Illegal instruction detected:
+// Operand has incorrect register class", a flat-to-private check -- and keep the
+// polynomial).
+// The unmasked collider builds on the transcendental unit too (round 6; round 5
+// kept them on the polynomial because the solve and evaluate kernels then disagreed
+// on contact decisions: the compiler's FMA contraction of the same frame code
+// differed between the kernels -- FitnessAcc::kPin now pins every rounding).  The
+// masked collider builds keep the polynomial, and carry the chains whose angles
+// reach beyond the unit's range (ChainHost::poly_trig).  0: round 5's builds.
 #ifndef IKPSO_COLLIDE_HW_TRIG
-#define IKPSO_COLLIDE_HW_TRIG 0  // experiment: the unmasked collider builds on the transcendental unit too
+#define IKPSO_COLLIDE_HW_TRIG 1
 #endif
 template <class Topo, int MODE, int TERMS>
 constexpr bool kHwTrigOk = IKPSO_FAST_HW_TRIG && MODE == IKPSO_ARITH_FAST && Topo::D <= 60 &&
-                           (!(TERMS & kTermColliders) || (IKPSO_COLLIDE_HW_TRIG && !(TERMS & kTermMask)));
+                           (!(TERMS & kTermColliders) ||
+                            (IKPSO_COLLIDE_HW_TRIG && !(TERMS & kTermMask) && !Topo::kGeneric));
 // The sin/cos flavour of a kernel build (sincos_fast): polynomial, hardware on
 // radians, or hardware on revolutions (kTermRev).
 template <class Topo, int MODE, int TERMS>
@@ -648,6 +717,10 @@ struct FitnessAcc {
     // Generic trees test a near node at once (hit): their deferred build hits a
     // hipcc 7.2 backend error (a flat-to-private check on the buffer's address).
     static constexpr bool kDefer = (TERMS & kTermColliders) && !Topo::kGeneric;
+    // FAST collider builds pin every rounding of the frames and of the fitness sums
+    // (child_frame_pinned_sc): the contact decisions of one arithmetic must not
+    // depend on the kernel that makes them
+    static constexpr bool kPin = (TERMS & kTermColliders) && MODE == IKPSO_ARITH_FAST;
     uint32_t near_mask;
     float* cand;
     bool hit;
@@ -676,7 +749,16 @@ struct FitnessAcc {
     {
         const int pk = Topo::kGeneric ? cc.parent[k] : Topo::parent(k);
         constexpr int HW = kHwTrig<Topo, MODE, TERMS>;
-        if (kOriginFrame<Topo, TERMS> && pk == 0) {
+        if constexpr (kPin) {  // FAST collider builds: every rounding pinned (child_frame_pinned_sc)
+            float sa, ca, sb, cb, sc, cc_;
+            sincos_fast<HW>(a, &sa, &ca);
+            sincos_fast<HW>(b, &sb, &cb);
+            sincos_fast<HW>(c, &sc, &cc_);
+            if (kOriginFrame<Topo, TERMS> && pk == 0)
+                F[k] = root_frame_pinned_sc(sa, ca, sb, cb, sc, cc_, link_len<HW>(cc, k));
+            else
+                F[k] = child_frame_pinned_sc(F[pk], sa, ca, sb, cb, sc, cc_, link_len<HW>(cc, k));
+        } else if (kOriginFrame<Topo, TERMS> && pk == 0) {
             float sa, ca, sb, cb, sc, cc_;
             sincos_fast<HW>(a, &sa, &ca);
             sincos_fast<HW>(b, &sb, &cb);
@@ -716,6 +798,8 @@ struct FitnessAcc {
         const float dx = rest3[0] - a, dy = rest3[1] - b, dz = rest3[2] - c;
         if constexpr (MODE == IKPSO_ARITH_REFERENCE) {
             rot_diff = rot_diff + ((dx * dx + dy * dy) + dz * dz);
+        } else if constexpr (kPin) {
+            rot_diff = rot_diff + __builtin_fmaf(dz, dz, __builtin_fmaf(dy, dy, dx * dx));
         } else {
 #pragma clang fp contract(fast)
             rot_diff = rot_diff + ((dx * dx + dy * dy) + dz * dz);
@@ -734,6 +818,8 @@ struct FitnessAcc {
             const float ez = F[k].pz - tgt3[2];
             if constexpr (MODE == IKPSO_ARITH_REFERENCE) {
                 distance = distance + ((ex * ex + ey * ey) + ez * ez) * cc.eff_w[k];
+            } else if constexpr (kPin) {
+                distance = __builtin_fmaf(__builtin_fmaf(ez, ez, __builtin_fmaf(ey, ey, ex * ex)), cc.eff_w[k], distance);
             } else {
 #pragma clang fp contract(fast)
                 distance = distance + ((ex * ex + ey * ey) + ez * ez) * cc.eff_w[k];

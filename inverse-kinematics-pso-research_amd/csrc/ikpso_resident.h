@@ -232,6 +232,25 @@ __host__ __device__ constexpr int kVelLds()
     return k <= 0 ? 0 : (k >= D ? D : (int)k);
 }
 
+// The collider builds' call (node_collides, out of line in FitnessAcc::finish) may
+// clobber SGPRs, so the chain constants the iteration keeps in SGPRs (loaded once
+// from the kernel arguments) are parked in VGPR lanes across it and read back with
+// v_readlane_b32 on the main path: 225 per iteration (round 5).  Re-reading them from
+// the kernarg segment every iteration instead -- through a pointer the compiler
+// cannot see is loop-invariant -- makes them scalar loads at their point of use.
+#ifndef IKPSO_COLLIDE_RELOAD
+#define IKPSO_COLLIDE_RELOAD 1
+#endif
+template <int J>
+__device__ __forceinline__ const ChainConsts<J>& kernarg_cc()
+{
+    // the chain constants are the kernels' first argument: offset 0 of the kernarg segment
+    const __attribute__((address_space(4))) char* p =
+        (const __attribute__((address_space(4))) char*)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(p));
+    return *(const ChainConsts<J>*)(const char*)p;
+}
+
 // Masked chains (kMasked builds): a locked dimension takes no draws and keeps
 // its rest value, as in the oracle's masked restatement.
 // KV: velocities held in LDS behind the local bests (kVelLds; the resident kernel)
@@ -387,7 +406,13 @@ __device__ __forceinline__ void swarm_resident_body(const ChainConsts<Topo::J>& 
     const PsoCoef coef = pso_coef(cc);
     for (int it = 0; it < io.iterations; ++it) {
         compiler_fence();
-        swarm_step<Topo, MODE, TERMS, BLOCK, KV>(cc, sh, s_pb, tid, x, v, pbf, coef, rng);
+        if constexpr ((TERMS & kTermColliders) && IKPSO_COLLIDE_RELOAD) {
+            // the chain constants re-read from the kernarg segment every iteration (kernarg_cc)
+            const ChainConsts<Topo::J>& cci = kernarg_cc<Topo::J>();
+            swarm_step<Topo, MODE, TERMS, BLOCK, KV>(cci, sh, s_pb, tid, x, v, pbf, pso_coef(cci), rng);
+        } else {
+            swarm_step<Topo, MODE, TERMS, BLOCK, KV>(cc, sh, s_pb, tid, x, v, pbf, coef, rng);
+        }
 
         // thrust::min_element + `globalMin > currentGlobalMin` (src/kernel.cu:315-323)
         const uint32_t bmin = swarm_argmin(sh, (it + 1) & 1, active ? ordered_key(pbf) : 0xFFFFFFFFu, &bidx);
@@ -569,8 +594,13 @@ inline hipError_t run_evaluate(const ChainHost& ch, const EvalIO& io, hipStream_
     int64_t blocks = (io.n + 255) / 256;
     if (blocks > 8192) blocks = 8192;
     if (blocks < 1) blocks = 1;
-    // the mask only places the given angles (no PSO): the unmasked builds evaluate it
-    if (ch.num_coll > 0)
+    // the mask only places the given angles (no PSO): the unmasked builds evaluate it -- but a chain whose
+    // angles reach beyond the transcendental unit's range (poly_trig) is solved by the masked collider
+    // builds for their polynomial sin/cos, and is evaluated by the same arithmetic
+    if (ch.poly_trig && IKPSO_COLLIDE_HW_TRIG)
+        hipLaunchKernelGGL((k_evaluate<Topo, MODE, kTermRuntime | kTermColliders | kTermMask>), dim3((unsigned)blocks),
+                           dim3(256), 0, stream, cc, io);
+    else if (ch.num_coll > 0)
         hipLaunchKernelGGL((k_evaluate<Topo, MODE, kTermRuntime | kTermColliders>), dim3((unsigned)blocks), dim3(256),
                            0, stream, cc, io);
     else

@@ -229,20 +229,22 @@ def test_collide_leg_tier_b(oracle, device, report):
     assert all(oracle.fitness(_with_targets(wl.chain, tg[b]), ang[b], colliders=shrunk) < FMAX for b in range(B))
 
 
-def test_collide_leg_reference_whole_solve(oracle, device):
+@pytest.mark.parametrize("kernel", ["resident", "auto"])
+def test_collide_leg_reference_whole_solve(oracle, device, kernel):
     """REFERENCE arithmetic over whole solves of the collide leg (500 iterations), the first
-    8 swarms of tests/golden/tierb_collide.npz: angles and fitness bit-identical to the
-    oracle's, so the improving-lanes filter changes no decision over a full solve."""
+    8 swarms of tests/golden/tierb_collide.npz, on the resident kernel and (AUTO: few swarms)
+    the cooperative latency variant: angles and fitness bit-identical to the oracle's, so
+    the improving-lanes filter changes no decision over a full solve."""
     from tierb import load_fixture
 
     wl = ikpso.workload(3)
     fx = load_fixture("collide")
     boxes = ikpso.init_colliders(4)[[0, 3]]
     B, P, I = 8, wl.particles, wl.iterations
-    s = ikpso.BatchSolver(wl.chain, P, pso=wl.pso, arith="reference", colliders=boxes)
+    s = ikpso.BatchSolver(wl.chain, P, pso=wl.pso, arith="reference", colliders=boxes, kernel=kernel)
     s.seed(B)
     ang, fit, res = (t.cpu().numpy() for t in s.solve(dev(wl.targets(0, B)), iterations=I))
-    assert "resident" in s.kernel, s.kernel
+    assert ("latency variant" in s.kernel) == (kernel == "auto"), s.kernel
     s.close()
     assert np.array_equal(ang, fx["ref_angles"][:B]) and np.array_equal(fit, fx["ref_fitness"][:B])
     assert np.max(np.abs(res - fx["ref_residual"][:B])) <= 1e-5

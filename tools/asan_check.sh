@@ -5,11 +5,11 @@
 # Device code is not instrumented (GPU ASan is not available on this pool), and
 # the kernel translation units are built without it: instrumenting their host
 # side left the 1024-lane kernels' launches returning success without running.
-#   tools/asan_check.sh build   -- here (CPU): builds vlib/asan/
+#   tools/asan_check.sh build   -- here (CPU): builds vlib6/asan/
 #   tools/asan_check.sh run     -- on the GPU box
 set -e
 ROOT="$(cd "$(dirname "$0")/.." && pwd)"
-OUT="$ROOT/vlib/asan"
+OUT="$ROOT/vlib6/asan"
 RT="$(dirname "$(/opt/rocm/llvm/bin/clang -print-file-name=libclang_rt.asan-x86_64.so 2>/dev/null)")"
 [ -d "$RT" ] || RT=/opt/rocm/llvm/lib/clang/22/lib/linux
 SAN="-Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined -Xarch_host -fno-omit-frame-pointer"

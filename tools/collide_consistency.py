@@ -20,8 +20,8 @@ import ikpso  # noqa: E402
 FMAX = np.float32(np.finfo(np.float32).max)
 
 
-def run(name, chain, boxes, tg, P, I, pso):
-    s = ikpso.BatchSolver(chain, P, pso=pso, colliders=boxes)
+def run(name, chain, boxes, tg, P, I, pso, kernel="auto"):
+    s = ikpso.BatchSolver(chain, P, pso=pso, colliders=boxes, kernel=kernel)
     B = len(tg)
     s.seed(B)
     t = torch.from_numpy(np.ascontiguousarray(tg)).cuda()
@@ -41,5 +41,10 @@ def run(name, chain, boxes, tg, P, I, pso):
 if __name__ == "__main__":
     wl = ikpso.workload(3)
     boxes = np.concatenate([ikpso.make_collider((0.6, 0.6, 0.6), (0.0, 0.9, -1.6)), ikpso.init_colliders(1)])
-    run("test_batch_with_colliders_fast", wl.chain, boxes, wl.targets(0, 32), 256, 40, ikpso.PSOConfig(0.5, 0.5, 1.25, 40))
-    run("collide_leg_64", wl.chain, ikpso.init_colliders(4)[[0, 3]], wl.targets(0, 64), 1024, 500, wl.pso)
+    for I in (0, 1, 5):
+        run(f"collide_leg_64_I{I}", wl.chain, ikpso.init_colliders(4)[[0, 3]], wl.targets(0, 64), 1024, I,
+            ikpso.PSOConfig(0.5, 0.5, 1.25, I), "resident")
+    for kernel in ("auto", "resident"):
+        run("test_batch_with_colliders_fast", wl.chain, boxes, wl.targets(0, 32), 256, 40,
+            ikpso.PSOConfig(0.5, 0.5, 1.25, 40), kernel)
+        run("collide_leg_64", wl.chain, ikpso.init_colliders(4)[[0, 3]], wl.targets(0, 64), 1024, 500, wl.pso, kernel)

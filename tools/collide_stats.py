@@ -6,7 +6,7 @@ counts, per solve, the box/collider pairs through the inline sphere test and
 how many pass it, the pairs through the quaternion sphere test, the GJK calls,
 their loop trips summed over lanes and over waves (the SIMD's view), and hits.
 
-  IKPSO_LIB=vlib/collide_stats.so IKPSO_ALLOW_STALE=1 \\
+  IKPSO_LIB=vlib6/collide_stats.so IKPSO_ALLOW_STALE=1 \\
       python tools/collide_stats.py [SWARMS] [ITERS] [SCENE] [OUT.json]
 
 SCENE: init03 (initColliders boxes 0 and 3, src/Main.cpp:537-559, which leave the

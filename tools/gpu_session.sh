@@ -20,7 +20,7 @@
 #   collconsist  FAST collider solve vs evaluate kernel (tools/collide_consistency.py; VLIBS = variants)
 #   collcmp      collider kernel ms, boxes near / far (tools/collide_cmp.sh; VARIANTS = product coll_vN ...)
 #   frame        the visualiser frame latency (tools/frame_bench.py)
-#   collstats    collider-term counters (tools/collide_stats.py) with vlib/collide_stats.so
+#   collstats    collider-term counters (tools/collide_stats.py) with vlib6/collide_stats.so
 #   frametrace   rocprofv3 kernel trace of the same (what device work one frame issues)
 #   var:<out>    interleaved variant timing (tools/gpu_var.sh; VAR_ARGS = "CONFIG SWARMS ITERS LIB...")
 #   asan         host-code ASan/UBSan run (tools/asan_check.sh)
@@ -70,15 +70,15 @@ for s in "$@"; do
       step hwprobe 120 tools/probes/hwtrig_bias gpurun_out/c5_angles.f32 gpurun_out/c3_angles.f32 || exit 11
       step hwcomp 600 python -u tools/hwtrig_comp.py ${HWCOMP_EPS:-} || exit 11 ;;
     collconsist)  # FAST collider solve vs evaluate kernel on the solve's answers (product, then VLIBS variants)
-      step collconsist_product 300 python -u tools/collide_consistency.py || exit 12
+      [ "${PRODUCT:-1}" = 0 ] || step collconsist_product 300 python -u tools/collide_consistency.py || exit 12
       for v in ${VLIBS:-}; do
-        IKPSO_LIB=vlib/$v.so IKPSO_ALLOW_STALE=1 step "collconsist_$v" 300 python -u tools/collide_consistency.py || exit 12
+        IKPSO_LIB=vlib6/$v.so IKPSO_ALLOW_STALE=1 step "collconsist_$v" 300 python -u tools/collide_consistency.py || exit 12
       done ;;
     collcmp) step collcmp 900 env VARIANTS="${VARIANTS:-product}" bash tools/collide_cmp.sh || exit 13 ;;
     frame) step frame 300 python tools/frame_bench.py || exit 7 ;;
-    collstats) [ -f vlib/collide_stats.so ] || { echo "no vlib/collide_stats.so"; exit 10; }
+    collstats) [ -f vlib6/collide_stats.so ] || { echo "no vlib6/collide_stats.so"; exit 10; }
       for sc in init03 far4 init4; do
-        IKPSO_LIB=vlib/collide_stats.so IKPSO_ALLOW_STALE=1 step "collstats_$sc" 300 \
+        IKPSO_LIB=vlib6/collide_stats.so IKPSO_ALLOW_STALE=1 step "collstats_$sc" 300 \
           python tools/collide_stats.py ${COLL_SWARMS:-1024} 500 $sc "gpurun_out/collide_stats_$sc.json" || exit 10
       done ;;
     frametrace)

@@ -10,9 +10,10 @@ to k; with an isotropic in-plane share of 2/3 that is an expected shrink of
 Here the scaled lengths are passed in the chain table itself (no rebuild), the
 FAST answers of the tier-B fixtures' swarms are solved for each eps, and the
 stated tests of tests/tierb.py are run on the GPU's reported fitness and on the
-oracle's fitness of the GPU's angles under the unscaled chain.  Test
-infrastructure: imports oracle/ as the checker.
-usage: hwtrig_comp.py [eps ...]  -> JSON lines"""
+oracle's fitness of the GPU's angles under the unscaled chain.  Since round 6 the
+library compensates by itself (kHwTrigAmplitudeBias, 3.23e-8): the eps given here
+then come on top of it.  Test infrastructure: imports oracle/ as the checker.
+usage: hwtrig_comp.py [--cfg 5,3,collide] [eps ...]  -> JSON lines"""
 import json
 import sys
 from pathlib import Path
@@ -37,13 +38,14 @@ def depths(chain):
 
 
 def run(cfg, eps):
-    wl = ikpso.workload(cfg)
+    wl = ikpso.workload(3 if cfg == "collide" else cfg)
     fx = load_fixture(cfg)
+    boxes = ikpso.init_colliders(4)[[0, 3]] if cfg == "collide" else None
     B, I = int(fx["swarms"]), wl.iterations
     ch = wl.chain.copy()
     ch["length"] = (ch["length"].astype(np.float64) * (1.0 + 2.0 * depths(ch) * eps)).astype(np.float32)
     s = ikpso.BatchSolver(ch, wl.particles, pso=ikpso.PSOConfig(0.5, 0.5, 1.25, I), limit_weight=wl.limit_weight,
-                          soft_lo=wl.soft_lo, soft_hi=wl.soft_hi)
+                          soft_lo=wl.soft_lo, soft_hi=wl.soft_hi, colliders=boxes)
     s.seed(B)
     tg = wl.targets(0, B)
     ang, fit, res = (t.cpu().numpy() for t in s.solve(torch.from_numpy(tg).cuda(), iterations=I))
@@ -54,7 +56,8 @@ def run(cfg, eps):
     for b in range(B):
         c = wl.chain.copy()
         c["target_position"][eff] = tg[b]
-        ofit[b] = oracle.fitness(c, ang[b], limit_weight=wl.limit_weight, soft_lo=wl.soft_lo, soft_hi=wl.soft_hi)
+        ofit[b] = oracle.fitness(c, ang[b], limit_weight=wl.limit_weight, soft_lo=wl.soft_lo, soft_hi=wl.soft_hi,
+                                 colliders=boxes)
     env = envelope(wl.chain, fx)
     rfit = fx["ref_fitness"]
     out = {"config": cfg, "eps": eps, "kernel": kern, "swarms": B}
@@ -67,7 +70,12 @@ def run(cfg, eps):
 
 
 if __name__ == "__main__":
-    eps_list = [float(a) for a in sys.argv[1:]] or [0.0, 2.7e-8, 3.23e-8]
-    for cfg in (5, 3):
+    args = sys.argv[1:]
+    cfgs = [5, 3]
+    if args and args[0] == "--cfg":
+        cfgs = [c if c == "collide" else int(c) for c in args[1].split(",")]
+        args = args[2:]
+    eps_list = [float(a) for a in args] or [0.0, 2.7e-8, 3.23e-8]
+    for cfg in cfgs:
         for eps in eps_list:
             print(json.dumps(run(cfg, eps)), flush=True)
