@@ -452,7 +452,8 @@ def summary(line: dict, value: float) -> dict:
     """Compact restatement of the line's figures (rounded), printed last."""
     r3 = lambda x: None if x is None else float(f"{x:.4g}")
     out = {"value": r3(value), "kernel_ms": line["roofline"].get("kernel_ms"),
-           "roofline_frac": line["roofline"].get("frac"), "single_solve_ms": r3(line.get("single_solve_ms"))}
+           "roofline_frac": line["roofline"].get("frac"), "single_solve_ms": r3(line.get("single_solve_ms")),
+           "single_solve_p10_ms": r3(line.get("single_solve_p10_ms"))}
     if line.get("frame"):
         out["frame_ms"] = {a: f["frame_ms"] for a, f in line["frame"].items()}
     if line.get("reference_arith"):
@@ -536,7 +537,7 @@ def main():
     ups_step = total * P * I
     value = ups_step * args.steps / elapsed
 
-    single_ms = None
+    single_ms = single_p10 = None
     if rank == 0 and cfg != 5 and colliders is None:
         s2 = ikpso.BatchSolver(wl.chain, P, pso=ikpso.PSOConfig(0.5, 0.5, 1.25, I), fit=wl.fit, arith=args.arith,
                                axis_mask=wl.axis_mask, fold=wl.fold)
@@ -544,13 +545,17 @@ def main():
         tg1 = targets[:1].contiguous()
         s2.solve(tg1, iterations=I)
         torch.cuda.synchronize()
+        # wall time of one solve to its answer on the host: the median of 50 (round 5 took 5, whose median
+        # moved 1.34 -> 1.46 ms between boxes while the kernel itself did not: profiles/r06/variant_timings/
+        # var_c2_r4_vs_cur.txt, round 4's build and this one interleaved, 1.375 vs 1.373 ms)
         ts = []
-        for _ in range(5):
+        for _ in range(50):
             a = time.perf_counter()
             r = s2.solve(tg1, iterations=I)
             r[0].cpu()
             ts.append(time.perf_counter() - a)
         single_ms = 1e3 * float(np.median(ts))
+        single_p10 = 1e3 * float(np.percentile(ts, 10))
         s2.close()
 
     # the REFERENCE-arithmetic (bit-identical to the oracle) throughput of the same workload, driver-measured
@@ -678,6 +683,7 @@ def main():
             },
             "solves_per_s": total * args.steps / elapsed,
             "single_solve_ms": single_ms,
+            "single_solve_p10_ms": single_p10,
             "roofline": roofline,
             "reference_arith": reference_arith,
             "legs": legs or None,

@@ -23,4 +23,6 @@ run valu --pmc SQ_INSTS_VALU SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_SALU SQ_INSTS_LDS 
 run fetch --pmc FETCH_SIZE
 run write --pmc WRITE_SIZE
 run cycles --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY
+# issue stalls on the LDS and the scalar/LDS instruction mix (round 6)
+run waits --pmc SQ_WAIT_INST_LDS SQ_WAIT_INST_ANY SQ_INSTS_SMEM SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES
 echo ALL_DONE

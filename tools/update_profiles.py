@@ -21,7 +21,9 @@ out_dir.mkdir(parents=True, exist_ok=True)
 src = ROOT / "gpurun_out"
 shutil.copy(src / f"{name}_trace" / "run_kernel_stats.csv", out_dir / f"{name}_kernel_stats.csv")
 counters = {}
-for pas in ("valu", "fetch", "write", "cycles"):
+for pas in ("valu", "fetch", "write", "cycles", "waits"):
+    if not (src / f"{name}_{pas}" / "run_counter_collection.csv").exists():  # (waits: round 6 on)
+        continue
     rows = list(csv.DictReader(open(src / f"{name}_{pas}" / "run_counter_collection.csv")))
     agg = collections.OrderedDict()
     for r in rows:

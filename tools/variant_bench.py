@@ -21,8 +21,9 @@ from ikpso import _abi
 def open_lib(path):
     lib = ctypes.CDLL(str(path))
     for name, (res, args) in _abi.SIGNATURES.items():
-        fn = getattr(lib, name)
-        fn.restype, fn.argtypes = res, args
+        fn = getattr(lib, name, None)  # (an older build may lack a newer introspection entry)
+        if fn is not None:
+            fn.restype, fn.argtypes = res, args
     return lib
 
 
