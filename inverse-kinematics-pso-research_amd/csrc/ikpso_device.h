@@ -880,13 +880,20 @@ struct FitnessAcc {
     // the pass made every value live across it a spill candidate, and the pass
     // paid for the spills whether or not a lane came near (round 5: the boxes out
     // of reach, 214 ms with the call in the pass vs 79 ms without it).
-    // `pbest`: the caller's local best, when the result only feeds the strict
-    // `f < pbest` update (updateLocalBests, src/kernel.cu:202-221).  A lane whose
-    // collision-free value is already >= a finite pbest cannot improve whether or not
-    // it collides (FLT_MAX is not < pbest either), so it skips the test and returns
-    // that value -- the update, and so every later state, is the same bit for bit.
-    // NaN (the default): every lane is tested, the value is the fitness itself.
-    __device__ __forceinline__ float finish(const ChainConsts<J>& cc, float pbest = __builtin_nanf("")) const
+    // finish(cc): the fitness itself (every lane tested).  finish_for_update(cc,
+    // pbest): a value valid ONLY for the strict `f < pbest` local-best update
+    // (updateLocalBests, src/kernel.cu:202-221) -- a lane whose collision-free value
+    // is already >= a finite pbest cannot improve whether or not it collides
+    // (FLT_MAX is not < pbest either), so it skips the test and returns that value:
+    // the update, and so every later state, is the same bit for bit, but the value
+    // itself may be the collision-free one.  A call site that keeps f as a fitness
+    // (an initial local best, a reported or evaluated fitness) must use finish(cc).
+    __device__ __forceinline__ float finish(const ChainConsts<J>& cc) const
+    {
+        return finish_for_update(cc, __builtin_nanf(""));  // NaN: no lane skips
+    }
+
+    __device__ __forceinline__ float finish_for_update(const ChainConsts<J>& cc, float pbest) const
     {
 #pragma clang fp contract(off)
         const float aw = angle_weight<TERMS>(cc);
@@ -1024,12 +1031,14 @@ struct FitnessAccDH {
         }
     }
 
-    __device__ __forceinline__ float finish(const ChainConsts<J>& cc, float = 0.0f) const  // (no collider term)
+    __device__ __forceinline__ float finish(const ChainConsts<J>& cc) const
     {
         float f = distance + angle_weight<TERMS>(cc) * rot_diff;
         if (penalty) f = f + limit_weight<TERMS>(cc) * pen;
         return f;
     }
+    // (no collider term: the value is the fitness itself; FitnessAcc::finish_for_update)
+    __device__ __forceinline__ float finish_for_update(const ChainConsts<J>& cc, float) const { return finish(cc); }
 };
 
 template <class Topo, int MODE, int TERMS>

@@ -337,7 +337,7 @@ __device__ __forceinline__ void swarm_step(const ChainConsts<Topo::J>& cc, Swarm
     }
 
     // updateLocalBests (src/kernel.cu:202-221): strict improvement
-    const float f = acc.finish(cc, pbf);
+    const float f = acc.finish_for_update(cc, pbf);
     if (f < pbf) {
         pbf = f;
 #pragma unroll

@@ -234,7 +234,7 @@ __global__ void __launch_bounds__(kStreamChunk) k_stream_step(const ChainConsts<
             for (int kn = J; kn >= 1; --kn) tb.back(cc, kn, node_trig<decltype(tb)::HW, A>(xs + A * (kn - 1)));
             f = tb.finish(cc, sh.tgt + 3 * (J - 1));
         } else {
-            f = acc.finish(cc, pbf);
+            f = acc.finish_for_update(cc, pbf);
         }
         // updateLocalBests (src/kernel.cu:202-221)
         // Whole-line stores only: a store covering part of a 128-B line makes
