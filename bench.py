@@ -543,16 +543,20 @@ def main():
                                axis_mask=wl.axis_mask, fold=wl.fold)
         s2.seed(1)
         tg1 = targets[:1].contiguous()
-        s2.solve(tg1, iterations=I)
+        out1 = (torch.empty((1, D), device=dev), torch.empty((1,), device=dev), torch.empty((1,), device=dev))
+        ans = torch.empty((1, D), dtype=torch.float32, pin_memory=True)  # the answer's host buffer, allocated once
+        s2.solve(tg1, iterations=I, out=out1)
         torch.cuda.synchronize()
         # wall time of one solve to its answer on the host: the median of 50 (round 5 took 5, whose median
         # moved 1.34 -> 1.46 ms between boxes while the kernel itself did not: profiles/r06/variant_timings/
         # var_c2_r4_vs_cur.txt, round 4's build and this one interleaved, 1.375 vs 1.373 ms)
         ts = []
+        stream = torch.cuda.current_stream()
         for _ in range(50):
             a = time.perf_counter()
-            r = s2.solve(tg1, iterations=I)
-            r[0].cpu()
+            s2.solve(tg1, iterations=I, out=out1)
+            ans.copy_(out1[0], non_blocking=True)
+            stream.synchronize()
             ts.append(time.perf_counter() - a)
         single_ms = 1e3 * float(np.median(ts))
         single_p10 = 1e3 * float(np.percentile(ts, 10))
