@@ -267,6 +267,43 @@ CollRec collider_record(const ikpso_collider& c)
     return r;
 }
 
+// The collider as an oriented box for the FAST separating-axis test (kFastSat): the
+// columns of the linear map quatRotVec(., q) (src/kernel.cu:1012-1037) -- the box's
+// axes -- computed in fp64, the half extents and the centre: box[0..8] = axes (axis
+// c at box[3c..3c+2]), box[9..11] = |x, y, z| / 2, box[12..14] = centre.  False when
+// the map is not a rotation to 1e-5 (a quaternion far from unit length makes the
+// reference's "box" a skewed parallelepiped): the FAST builds then test it by GJK.
+bool collider_box(const ikpso_collider& c, float* box)
+{
+    const double x = c.quat[0], y = c.quat[1], z = c.quat[2], w = c.quat[3];
+    double m[3][3];  // m[row][col]: quatRotVec(e_col)
+    for (int col = 0; col < 3; ++col) {
+        const double v[3] = {col == 0 ? 1.0 : 0.0, col == 1 ? 1.0 : 0.0, col == 2 ? 1.0 : 0.0};
+        const double c1x = y * v[2] - z * v[1] + w * v[0], c1y = z * v[0] - x * v[2] + w * v[1],
+                     c1z = x * v[1] - y * v[0] + w * v[2];
+        const double c2x = y * c1z - z * c1y, c2y = z * c1x - x * c1z, c2z = x * c1y - y * c1x;
+        m[0][col] = v[0] + 2.0 * c2x;
+        m[1][col] = v[1] + 2.0 * c2y;
+        m[2][col] = v[2] + 2.0 * c2z;
+    }
+    bool ortho = true;
+    for (int a = 0; a < 3; ++a)
+        for (int b = 0; b < 3; ++b) {
+            const double d = m[0][a] * m[0][b] + m[1][a] * m[1][b] + m[2][a] * m[2][b];
+            ortho = ortho && fabs(d - (a == b ? 1.0 : 0.0)) <= 1e-5;
+        }
+    for (int col = 0; col < 3; ++col)
+        for (int row = 0; row < 3; ++row) box[3 * col + row] = (float)m[row][col];
+    box[9] = 0.5f * fabsf(c.x);
+    box[10] = 0.5f * fabsf(c.y);
+    box[11] = 0.5f * fabsf(c.z);
+    box[12] = c.pos[0];
+    box[13] = c.pos[1];
+    box[14] = c.pos[2];
+    box[15] = 0.0f;
+    return ortho;
+}
+
 ikpso_status parse_chain(const std::vector<ikpso_node>& nodes, const ikpso_pso_config& pso,
                          const ikpso_fitness_config& fit, const Extras& ex, ChainHost& ch)
 {
@@ -351,7 +388,8 @@ ikpso_status parse_chain(const std::vector<ikpso_node>& nodes, const ikpso_pso_c
     ch.num_coll = ex.collider_count;
     ch.coll_off = ((size_t)10 * J + 15) & ~size_t(15);
     ch.coll_lim_off = ch.coll_off + (size_t)16 * ch.num_coll;
-    ch.aux.assign(ch.coll_lim_off + (size_t)J * ch.num_coll, 0.0f);
+    ch.coll_box_off = (ch.coll_lim_off + (size_t)J * ch.num_coll + 15) & ~size_t(15);
+    ch.aux.assign(ch.coll_box_off + (size_t)16 * ch.num_coll, 0.0f);
     // near_collider's limit for node k and collider c (ikpso_collide.h): one sphere around
     // the node's link box and node box, centred at the link's midpoint, that any box pair
     // node_collides would test lies within.  Every node position is within
@@ -365,6 +403,7 @@ ikpso_status parse_chain(const std::vector<ikpso_node>& nodes, const ikpso_pso_c
     for (int i = 0; i < ch.num_coll; ++i) {
         const CollRec r = collider_record(ex.colliders[i]);
         memcpy(ch.aux.data() + ch.coll_off + 16 * (size_t)i, &r, sizeof(r));
+        ch.coll_obb = ch.coll_obb && collider_box(ex.colliders[i], ch.aux.data() + ch.coll_box_off + 16 * (size_t)i);
         if (!std::isfinite(r.radius) || !std::isfinite(r.px) || !std::isfinite(r.py) || !std::isfinite(r.pz))
             return IKPSO_ERR_INVALID_ARG;
         const double c1 = fabs((double)r.px) + fabs((double)r.py) + fabs((double)r.pz);

@@ -449,6 +449,81 @@ __device__ __forceinline__ bool near_collider(float nx, float ny, float nz, floa
     return near;
 }
 
+// FAST: the exact overlap test of two oriented boxes by separating axes (Gottschalk's
+// OBB test: the 3 + 3 face axes and the 9 edge-pair axes), in place of GJK.  a, b:
+// centres; A, B: axes (axis i at [3i..3i+2], unit); ea, eb: half extents.  Fixed
+// work and no divergence (GJK: ~2.3 iterations at 0.56 SIMT efficiency, round 5) and
+// no quaternion.  Exact in exact arithmetic; GJK's tolerance (a hit once the origin
+// is within sqrt(FLT_EPSILON) of a simplex of support points) also counts boxes
+// within ~3.5e-4 of touching, so the two may decide differently inside that band
+// (the stated FAST tolerances: tests/test_gpu_collide.py).  The 1e-6 added to
+// |R| guards near-parallel edge pairs (a degenerate cross axis then cannot separate).
+__device__ __forceinline__ bool obb_overlap(const float a[3], const float A[9], const float ea[3], const float b[3],
+                                            const float B[9], const float eb[3])
+{
+    float R[3][3], AR[3][3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            R[i][j] = (A[3 * i] * B[3 * j] + A[3 * i + 1] * B[3 * j + 1]) + A[3 * i + 2] * B[3 * j + 2];
+            AR[i][j] = fabsf(R[i][j]) + 1e-6f;
+        }
+    const float d0 = b[0] - a[0], d1 = b[1] - a[1], d2 = b[2] - a[2];
+    float t[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) t[i] = (d0 * A[3 * i] + d1 * A[3 * i + 1]) + d2 * A[3 * i + 2];
+    bool sep = false;
+#pragma unroll
+    for (int i = 0; i < 3; ++i)  // A's face axes
+        sep = sep || fabsf(t[i]) > ea[i] + ((eb[0] * AR[i][0] + eb[1] * AR[i][1]) + eb[2] * AR[i][2]);
+#pragma unroll
+    for (int j = 0; j < 3; ++j)  // B's face axes
+        sep = sep || fabsf((t[0] * R[0][j] + t[1] * R[1][j]) + t[2] * R[2][j]) >
+                         ((ea[0] * AR[0][j] + ea[1] * AR[1][j]) + ea[2] * AR[2][j]) + eb[j];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {  // edge pairs A_i x B_j
+        const int i1 = (i + 1) % 3, i2 = (i + 2) % 3;
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            const int j1 = (j + 1) % 3, j2 = (j + 2) % 3;
+            const float ra = ea[i1] * AR[i2][j] + ea[i2] * AR[i1][j];
+            const float rb = eb[j1] * AR[i][j2] + eb[j2] * AR[i][j1];
+            sep = sep || fabsf(t[i2] * R[i1][j] - t[i1] * R[i2][j]) > ra + rb;
+        }
+    }
+    return !sep;
+}
+
+// The collider block for one node with the separating-axis test (FAST, kFastSat):
+// the node box and the link box (src/kernel.cu:104-118) oriented by the node's world
+// rotation (the frame itself: matrixToQuaternion + quatRotVec of an orthonormal
+// frame is the frame), against every collider box (ChainConsts::coll_box), each pair
+// behind node_collides' sphere test with the gain's bound.
+__device__ __forceinline__ bool node_collides_obb(float r00, float r01, float r02, float r10, float r11, float r12,
+                                                  float r20, float r21, float r22, float nx, float ny, float nz,
+                                                  float ex, float ey, float ez, float length, const CollRec* coll,
+                                                  const float* cbox, int count)
+{
+    const float A[9] = {r00, r10, r20, r01, r11, r21, r02, r12, r22};  // the frame's columns
+    const float pn[3] = {nx, ny, nz};
+    const float pl[3] = {(nx + ex) * 0.5f, (ny + ey) * 0.5f, (nz + ez) * 0.5f};
+    const float en[3] = {kGizmo * 0.5f, kGizmo * 0.5f, kGizmo * 0.5f};
+    const float el[3] = {fabsf(length) * 0.5f, kGizmo * 0.125f, kGizmo * 0.125f};
+    const float rn = sphere_radius(kGizmo, kGizmo, kGizmo, kGainBound);
+    const float rl = sphere_radius(length, kGizmo * 0.25f, kGizmo * 0.25f, kGainBound);
+    bool hit = false;
+    for (int i = 0; i < count && !hit; ++i) {
+        const CollRec& c = coll[i];
+        const float* bx = cbox + 16 * i;
+        if (may_touch(pn[0], pn[1], pn[2], rn, c.px, c.py, c.pz, c.radius))
+            hit = obb_overlap(pn, A, en, bx + 12, bx, bx + 9);
+        if (!hit && may_touch(pl[0], pl[1], pl[2], rl, c.px, c.py, c.pz, c.radius))
+            hit = obb_overlap(pl, A, el, bx + 12, bx, bx + 9);
+    }
+    return hit;
+}
+
 // The collider block of calculateDistance for one node (src/kernel.cu:104-136):
 // node box (GIZMO cube at the node) and link box (length x GIZMO/4 x GIZMO/4,
 // centred between node and parent), both oriented by the node's world

@@ -649,6 +649,16 @@ using RngFor = XorwowT<!(TERMS & kTermColliders)>;
 #ifndef IKPSO_COLLIDE_HW_TRIG
 #define IKPSO_COLLIDE_HW_TRIG 1
 #endif
+// FAST collider builds test the near nodes by separating axes (node_collides_obb) instead
+// of the reference's GJK: the same routing as the transcendental unit's (unmasked, compiled
+// topologies); the host sends chains whose colliders are not rotations to the masked builds
+// (ChainHost::coll_obb).  0: GJK in every build.
+#ifndef IKPSO_FAST_SAT
+#define IKPSO_FAST_SAT 1
+#endif
+template <class Topo, int MODE, int TERMS>
+constexpr bool kFastSat = IKPSO_FAST_SAT && MODE == IKPSO_ARITH_FAST && (TERMS & kTermColliders) &&
+                          !(TERMS & kTermMask) && !Topo::kGeneric;
 template <class Topo, int MODE, int TERMS>
 constexpr bool kHwTrigOk = IKPSO_FAST_HW_TRIG && MODE == IKPSO_ARITH_FAST && Topo::D <= 60 &&
                            (!(TERMS & kTermColliders) ||
@@ -905,8 +915,14 @@ struct FitnessAcc {
             while (m != 0u) {
                 const float* c = cand + 16 * __builtin_ctz(m);
                 m &= m - 1u;
-                if (node_collides(c[0], c[1], c[2], c[3], c[4], c[5], c[6], c[7], c[8], c[9], c[10], c[11], c[12],
-                                  c[13], c[14], c[15], cc.coll, cc.num_coll IKPSO_CC_STATS)) {
+                if constexpr (kFastSat<Topo, MODE, TERMS>) {
+                    if (node_collides_obb(c[0], c[1], c[2], c[3], c[4], c[5], c[6], c[7], c[8], c[9], c[10], c[11],
+                                          c[12], c[13], c[14], c[15], cc.coll, cc.coll_box, cc.num_coll)) {
+                        f = FLT_MAX;
+                        break;
+                    }
+                } else if (node_collides(c[0], c[1], c[2], c[3], c[4], c[5], c[6], c[7], c[8], c[9], c[10], c[11],
+                                         c[12], c[13], c[14], c[15], cc.coll, cc.num_coll IKPSO_CC_STATS)) {
                     f = FLT_MAX;
                     break;
                 }

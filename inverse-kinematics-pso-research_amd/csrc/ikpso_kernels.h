@@ -72,6 +72,9 @@ struct ChainHost {
     bool colliders_far = false;   // the scene has colliders, none within the arm's reach (parse_chain)
     size_t coll_off = 0;          // float offset of the collider records in aux
     size_t coll_lim_off = 0;      // ... of near_collider's squared limits [J][num_coll] (after the records)
+    size_t coll_box_off = 0;      // ... of the colliders as oriented boxes [num_coll][16] (after the limits)
+    bool coll_obb = true;         // every collider's quaternion is a rotation (|q| = 1 to 1e-5): the FAST
+                                  // builds may test it as an oriented box (kFastSat); else they take GJK
     // joint-axis mask over the kernel's dimensions (all set: no mask) and the
     // number of free dimensions, which is the API's D
     uint64_t free_mask = 0;
@@ -221,6 +224,7 @@ ChainConsts<J> make_consts(const ChainHost& h)
     c.num_coll = h.num_coll;
     c.coll = h.num_coll && h.aux_dev ? reinterpret_cast<const CollRec*>(h.aux_dev + h.coll_off) : nullptr;
     c.coll_lim = h.num_coll && h.aux_dev ? h.aux_dev + h.coll_lim_off : nullptr;
+    c.coll_box = h.num_coll && h.aux_dev ? h.aux_dev + h.coll_box_off : nullptr;
     c.coll_stats = collide_stats_buffer();
     c.free_mask = h.free_mask;
     c.dfree = h.dfree;

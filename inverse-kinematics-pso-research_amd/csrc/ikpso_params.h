@@ -43,6 +43,8 @@ struct ChainConsts {
     int32_t num_coll;         // colliders (kTermColliders kernels only)
     const struct CollRec* coll;  // [num_coll] device records, inside the aux buffer
     const float* coll_lim;    // [J][num_coll] near_collider's squared limits, inside the aux buffer
+    const float* coll_box;    // [num_coll][16] the colliders as oriented boxes (FAST separating-axis test,
+                              // kFastSat): axes (3 columns), half extents, centre; inside the aux buffer
     unsigned long long* coll_stats;  // IKPSO_COLLIDE_STATS builds: [kCsCount] counters (else null)
     // Joint-axis mask (extension): bit d set when kernel
     // dimension d is a PSO dimension; dfree = popcount.  The kernels of the

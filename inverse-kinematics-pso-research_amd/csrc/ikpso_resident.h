@@ -597,7 +597,7 @@ inline hipError_t run_evaluate(const ChainHost& ch, const EvalIO& io, hipStream_
     // the mask only places the given angles (no PSO): the unmasked builds evaluate it -- but a chain whose
     // angles reach beyond the transcendental unit's range (poly_trig) is solved by the masked collider
     // builds for their polynomial sin/cos, and is evaluated by the same arithmetic
-    if (ch.poly_trig && IKPSO_COLLIDE_HW_TRIG)
+    if ((ch.poly_trig && IKPSO_COLLIDE_HW_TRIG) || (ch.num_coll > 0 && !ch.coll_obb))
         hipLaunchKernelGGL((k_evaluate<Topo, MODE, kTermRuntime | kTermColliders | kTermMask>), dim3((unsigned)blocks),
                            dim3(256), 0, stream, cc, io);
     else if (ch.num_coll > 0)

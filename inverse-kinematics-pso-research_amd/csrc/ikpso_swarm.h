@@ -259,7 +259,7 @@ inline hipError_t with_runtime_terms(const ChainHost& ch, F&& f)
         const bool coll = ch.num_coll > 0 || ch.poly_trig;
         // (IKPSO_COLLIDE_HW_TRIG: the unmasked collider builds use the transcendental unit,
         // so a wide-angle chain takes the masked build, whose sin/cos is the polynomial)
-        if (coll && (ch.masked || (IKPSO_COLLIDE_HW_TRIG && ch.poly_trig)))
+        if (coll && (ch.masked || (IKPSO_COLLIDE_HW_TRIG && ch.poly_trig) || (ch.num_coll > 0 && !ch.coll_obb)))
             return f(std::integral_constant<int, kTermRuntime | kTermColliders | kTermMask>{});
         if (coll) return f(std::integral_constant<int, kTermRuntime | kTermColliders>{});
         if (ch.masked) return f(std::integral_constant<int, kTermRuntime | kTermMask>{});
