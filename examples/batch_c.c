@@ -1,7 +1,9 @@
 /* batch_c.c -- the batched C ABI (include/ikpso.h) from plain C: B independent
  * IK targets for the reference arm (src/Main.cpp:76-116), one launch.
  * HIP's C runtime API for device memory; no torch, no Python.
- * usage: batch_c [B] [iterations] */
+ * usage: batch_c [B] [iterations] [colliders]
+ *   colliders: the reference's initColliders boxes 0 and 3 (src/Main.cpp:537-559) and a
+ *   third box out of the arm's reach (the collider term, its host-side early-out) */
 #include <hip/hip_runtime_api.h>
 #include <math.h>
 #include <stdio.h>
@@ -80,6 +82,18 @@ int main(int argc, char** argv)
     desc.pso.iterations = iters;
     desc.fit.angle_weight = 3.0f;
     desc.fit.error_threshold = 0.1f;
+    ikpso_collider boxes[3];
+    memset(boxes, 0, sizeof(boxes));
+    if (argc > 3 && strcmp(argv[3], "colliders") == 0) {
+        static const float pos[3][3] = {{1.0f, 0.0f, 0.0f}, {0.0f, 0.0f, 1.0f}, {40.0f, 0.0f, 0.0f}};
+        for (int i = 0; i < 3; ++i) {
+            boxes[i].x = boxes[i].y = boxes[i].z = 1.0f;
+            for (int c = 0; c < 3; ++c) boxes[i].pos[c] = pos[i][c];
+            boxes[i].quat[3] = 1.0f;
+        }
+        desc.colliders = boxes;
+        desc.collider_count = 3;
+    }
     ikpso_solver* s;
     CHECK_IK(ikpso_solver_create(&desc, &s));
     CHECK_IK(ikpso_solver_seed(s, B, 0, 0, NULL));
@@ -107,7 +121,8 @@ int main(int argc, char** argv)
     }
     printf("kernel %s: %d swarms x %d particles x %d iterations in %.3f ms = %.3e particle-updates/s\n",
            ikpso_solver_kernel_name(s), B, P, iters, ms, (double)B * P * iters / (ms * 1e-3));
-    printf("mean fitness %.6f, mean residual %.6f, finite %d\n", mf / B, mr / B, finite);
+    printf("mean fitness %.6f, mean residual %.6f, finite %d, colliders tested %d\n", mf / B, mr / B, finite,
+           ikpso_solver_collider_count(s));
     ikpso_solver_destroy(s);
     return finite ? 0 : 2;
 }

@@ -270,9 +270,11 @@ CollRec collider_record(const ikpso_collider& c)
 // The collider as an oriented box for the FAST separating-axis test (kFastSat): the
 // columns of the linear map quatRotVec(., q) (src/kernel.cu:1012-1037) -- the box's
 // axes -- computed in fp64, the half extents and the centre: box[0..8] = axes (axis
-// c at box[3c..3c+2]), box[9..11] = |x, y, z| / 2, box[12..14] = centre.  False when
-// the map is not a rotation to 1e-5 (a quaternion far from unit length makes the
-// reference's "box" a skewed parallelepiped): the FAST builds then test it by GJK.
+// c at box[3c..3c+2], normalised), box[9..11] = |x, y, z| / 2 times the columns'
+// lengths, box[12..14] = centre.  A quaternion a little off unit length (the
+// reference's initColliders box 1 has |q|^2 = 1.0001) makes the map a rotation scaled
+// and skewed by ~|q|^2 - 1: below 1e-3 that moves the box's faces by less than GJK's
+// own ~3.5e-4 tolerance band; beyond it (false) the FAST builds test it by GJK.
 bool collider_box(const ikpso_collider& c, float* box)
 {
     const double x = c.quat[0], y = c.quat[1], z = c.quat[2], w = c.quat[3];
@@ -290,13 +292,15 @@ bool collider_box(const ikpso_collider& c, float* box)
     for (int a = 0; a < 3; ++a)
         for (int b = 0; b < 3; ++b) {
             const double d = m[0][a] * m[0][b] + m[1][a] * m[1][b] + m[2][a] * m[2][b];
-            ortho = ortho && fabs(d - (a == b ? 1.0 : 0.0)) <= 1e-5;
+            ortho = ortho && fabs(d - (a == b ? 1.0 : 0.0)) <= 1e-3;
         }
-    for (int col = 0; col < 3; ++col)
-        for (int row = 0; row < 3; ++row) box[3 * col + row] = (float)m[row][col];
-    box[9] = 0.5f * fabsf(c.x);
-    box[10] = 0.5f * fabsf(c.y);
-    box[11] = 0.5f * fabsf(c.z);
+    const double half[3] = {0.5 * fabs((double)c.x), 0.5 * fabs((double)c.y), 0.5 * fabs((double)c.z)};
+    for (int col = 0; col < 3; ++col) {
+        const double n = sqrt(m[0][col] * m[0][col] + m[1][col] * m[1][col] + m[2][col] * m[2][col]);
+        ortho = ortho && n > 0.0;
+        for (int row = 0; row < 3; ++row) box[3 * col + row] = (float)(n > 0.0 ? m[row][col] / n : 0.0);
+        box[9 + col] = (float)(half[col] * n);
+    }
     box[12] = c.pos[0];
     box[13] = c.pos[1];
     box[14] = c.pos[2];

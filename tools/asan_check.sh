@@ -28,6 +28,7 @@ run)
   export ASAN_OPTIONS=detect_leaks=0:halt_on_error=1:abort_on_error=0 UBSAN_OPTIONS=halt_on_error=1:print_stacktrace=1
   timeout -k 10 120 "$OUT/compat_frames" 3 16384
   timeout -k 10 120 "$OUT/batch_c" 64 100
+  timeout -k 10 120 "$OUT/batch_c" 16 50 colliders  # collider boxes, the separating-axis path, the reach test
   timeout -k 10 120 "$OUT/compat_frames" 2 300    # ragged particle count (resident / latency paths)
   timeout -k 10 120 "$OUT/compat_frames" replay 3 2 1024  # the recorded-session replay mode
   echo ASAN_CLEAN
