@@ -269,10 +269,11 @@ ikpso_status ikpso_solver_generator_states(ikpso_solver* solver, int64_t first_s
 /* Introspection.  dof = D, the free dimensions. */
 int ikpso_solver_dof(const ikpso_solver* solver);
 int ikpso_solver_effectors(const ikpso_solver* solver);
-/* Colliders the solver's kernels test: the descriptor's collider_count, or 0 when
- * none lies within the arm's reach of any node (the term can then never
- * contribute, and the chain is solved by the kernels without it; the environment
- * variable IKPSO_KEEP_FAR_COLLIDERS=1 keeps it). */
+/* Colliders the solver's kernels test: those of the descriptor's colliders that lie
+ * within the arm's reach of some node (one beyond it can never touch the arm, so it
+ * can never change a fitness); with none left the chain is solved by the kernels
+ * without the collider term.  The environment variable IKPSO_KEEP_FAR_COLLIDERS=1
+ * keeps every collider. */
 int ikpso_solver_collider_count(const ikpso_solver* solver);
 /* Name of the kernel variant the solver dispatches to (family / topology); after a
  * solve_batch that AUTO routed to the cooperative latency variant (a few swarms),

@@ -388,29 +388,45 @@ ikpso_status parse_chain(const std::vector<ikpso_node>& nodes, const ikpso_pso_c
     ch.use_posref = fit.distance_weight != 0.0f;
     ch.lim_w = ex.limit_weight;
     ch.use_penalty = ex.limit_weight != 0.0f && ex.soft_lo && ex.soft_hi;
-    // aux = [posref 4J | soft_lo 3J | soft_hi 3J | pad to 16 floats | collider records]
-    ch.num_coll = ex.collider_count;
-    ch.coll_off = ((size_t)10 * J + 15) & ~size_t(15);
-    ch.coll_lim_off = ch.coll_off + (size_t)16 * ch.num_coll;
-    ch.coll_box_off = (ch.coll_lim_off + (size_t)J * ch.num_coll + 15) & ~size_t(15);
-    ch.aux.assign(ch.coll_box_off + (size_t)16 * ch.num_coll, 0.0f);
+    // aux = [posref 4J | soft_lo 3J | soft_hi 3J | pad to 16 floats | collider records | near limits |
+    //        collider boxes], the colliders being those within the arm's reach (below)
+    //
     // near_collider's limit for node k and collider c (ikpso_collide.h): one sphere around
     // the node's link box and node box, centred at the link's midpoint, that any box pair
     // node_collides would test lies within.  Every node position is within
     // |origin| + sum |len| of the frame's origin (a bound on the exact test's |centre|_1
     // margin term through |a|_1 <= sqrt(3) |a|).
+    //
+    // Host-side pruning: every node (and link midpoint) lies within the arm's length sum
+    // sum_k |len_k| of the origin's position, so a collider farther from it than that plus
+    // near_collider's limit for every node can never pass the inline sphere test, let
+    // alone the exact one (the margin covers the fp32 FK's rounding, ~1e-6 of the reach):
+    // it can never contribute to any fitness, and is left out.  With none left the chain
+    // is solved without the term, by the plain kernels -- bit-identical answers in
+    // REFERENCE arithmetic (the same reference operation order), and in FAST the plain
+    // kernels' own arithmetic.  IKPSO_KEEP_FAR_COLLIDERS=1 keeps every collider (to time
+    // the collider kernels with nothing near).
     double reach = sqrt((double)ch.m0[3] * ch.m0[3] + (double)ch.m0[7] * ch.m0[7] + (double)ch.m0[11] * ch.m0[11]);
-    for (int k = 1; k <= J; ++k) reach += fabs((double)ch.len[k]);
-    reach *= 1.001;
+    double arm = 0.0;
+    for (int k = 1; k <= J; ++k) arm += fabs((double)ch.len[k]);
+    reach = (reach + arm) * 1.001;
     const double gb = (double)kGainBound, lw = (double)kGizmo * 0.25;
     const double rn = 0.5 * sqrt(3.0) * (double)kGizmo * gb;
-    for (int i = 0; i < ch.num_coll; ++i) {
-        const CollRec r = collider_record(ex.colliders[i]);
-        memcpy(ch.aux.data() + ch.coll_off + 16 * (size_t)i, &r, sizeof(r));
-        ch.coll_obb = ch.coll_obb && collider_box(ex.colliders[i], ch.aux.data() + ch.coll_box_off + 16 * (size_t)i);
+    const int nin = ex.collider_count;
+    std::vector<CollRec> recs(nin);
+    std::vector<float> lims((size_t)nin * J);
+    std::vector<int> kept;
+    const char* keep = getenv("IKPSO_KEEP_FAR_COLLIDERS");
+    const bool keep_all = keep && keep[0] == '1';
+    for (int i = 0; i < nin; ++i) {
+        const CollRec r = recs[i] = collider_record(ex.colliders[i]);
         if (!std::isfinite(r.radius) || !std::isfinite(r.px) || !std::isfinite(r.py) || !std::isfinite(r.pz))
             return IKPSO_ERR_INVALID_ARG;
         const double c1 = fabs((double)r.px) + fabs((double)r.py) + fabs((double)r.pz);
+        const double dx = (double)r.px - ch.m0[3], dy = (double)r.py - ch.m0[7], dz = (double)r.pz - ch.m0[11];
+        const double dist = sqrt(dx * dx + dy * dy + dz * dz);
+        const double margin = 1e-3 + 1e-4 * (arm + dist + c1);
+        bool reachable = false;
         for (int k = 1; k <= J; ++k) {
             const double len = fabs((double)ch.len[k]);
             const double rl = 0.5 * sqrt(len * len + 2.0 * lw * lw) * gb;
@@ -418,35 +434,23 @@ ikpso_status parse_chain(const std::vector<ikpso_node>& nodes, const ikpso_pso_c
             const double reach_kc = rk + (double)r.radius;
             const double lim = (reach_kc + 1e-3 + 1e-4 * (sqrt(3.0) * reach + c1 + reach_kc)) * 1.0001;
             if (!std::isfinite(lim)) return IKPSO_ERR_INVALID_ARG;
-            ch.aux[ch.coll_lim_off + (size_t)(k - 1) * ch.num_coll + i] = (float)(lim * lim);
+            lims[(size_t)i * J + (k - 1)] = (float)(lim * lim);
+            reachable = reachable || dist - arm <= sqrt((double)lims[(size_t)i * J + (k - 1)]) + margin;
         }
+        if (reachable || keep_all) kept.push_back(i);
     }
-    // Host-side early-out: every node (and link midpoint) lies within the arm's length
-    // sum_k |len_k| of the origin's position, so a collider farther from it than that
-    // plus near_collider's limit for every node can never pass the inline sphere test,
-    // let alone GJK (the margin covers the fp32 FK's rounding, ~1e-6 of the reach).
-    // When that holds for every collider the term contributes nothing to any fitness:
-    // the chain is solved without it, by the plain kernels -- bit-identical answers in
-    // REFERENCE arithmetic (the same reference operation order), and in FAST the
-    // plain kernels' own arithmetic.  IKPSO_KEEP_FAR_COLLIDERS=1 keeps the term (to
-    // time the collider kernels with nothing near).
-    if (ch.num_coll > 0) {
-        double arm = 0.0;
-        for (int k = 1; k <= J; ++k) arm += fabs((double)ch.len[k]);
-        bool reachable = false;
-        for (int i = 0; i < ch.num_coll && !reachable; ++i) {
-            const CollRec r = collider_record(ex.colliders[i]);
-            const double dx = (double)r.px - ch.m0[3], dy = (double)r.py - ch.m0[7], dz = (double)r.pz - ch.m0[11];
-            const double dist = sqrt(dx * dx + dy * dy + dz * dz);
-            const double margin = 1e-3 + 1e-4 * (arm + dist + fabs((double)r.px) + fabs((double)r.py) + fabs((double)r.pz));
-            for (int k = 1; k <= J && !reachable; ++k) {
-                const double lim = sqrt((double)ch.aux[ch.coll_lim_off + (size_t)(k - 1) * ch.num_coll + i]);
-                reachable = dist - arm <= lim + margin;
-            }
-        }
-        const char* keep = getenv("IKPSO_KEEP_FAR_COLLIDERS");
-        ch.colliders_far = !reachable;
-        if (!reachable && !(keep && keep[0] == '1')) ch.num_coll = 0;
+    ch.colliders_dropped = nin - (int)kept.size();
+    ch.num_coll = (int)kept.size();
+    ch.coll_off = ((size_t)10 * J + 15) & ~size_t(15);
+    ch.coll_lim_off = ch.coll_off + (size_t)16 * ch.num_coll;
+    ch.coll_box_off = (ch.coll_lim_off + (size_t)J * ch.num_coll + 15) & ~size_t(15);
+    ch.aux.assign(ch.coll_box_off + (size_t)16 * ch.num_coll, 0.0f);
+    for (int j = 0; j < ch.num_coll; ++j) {
+        const int i = kept[j];
+        memcpy(ch.aux.data() + ch.coll_off + 16 * (size_t)j, &recs[i], sizeof(CollRec));
+        ch.coll_obb = ch.coll_obb && collider_box(ex.colliders[i], ch.aux.data() + ch.coll_box_off + 16 * (size_t)j);
+        for (int k = 1; k <= J; ++k)
+            ch.aux[ch.coll_lim_off + (size_t)(k - 1) * ch.num_coll + j] = lims[(size_t)i * J + (k - 1)];
     }
     if (ch.use_posref && ex.positions)
         for (int i = 0; i < 4 * J; ++i) ch.aux[i] = ex.positions[i + (ex.posref_node_slot ? 8 : 0)];

@@ -68,8 +68,8 @@ struct ChainHost {
     bool unit_rev_bounds = false; // ... and they are [0, 1] in revolutions (kTermUnitBounds): [0, 2pi]
     bool ordered_bounds = false;  // ... and finite with lo <= hi (REFERENCE uniform builds: median clamp)
     bool sym_penalty = false;     // soft limits symmetric and within a revolution of the clamp (kTermSymPenalty)
-    int num_coll = 0;             // colliders (obj_t) of the scene; 0 when none is within reach
-    bool colliders_far = false;   // the scene has colliders, none within the arm's reach (parse_chain)
+    int num_coll = 0;             // colliders (obj_t) of the scene within the arm's reach (parse_chain)
+    int colliders_dropped = 0;    // ... and those left out, beyond it
     size_t coll_off = 0;          // float offset of the collider records in aux
     size_t coll_lim_off = 0;      // ... of near_collider's squared limits [J][num_coll] (after the records)
     size_t coll_box_off = 0;      // ... of the colliders as oriented boxes [num_coll][16] (after the limits)

@@ -255,9 +255,11 @@ def test_collide_leg_reference_whole_solve(oracle, device, kernel):
 
 @pytest.mark.parametrize("arith", ["reference", "fast"])
 def test_far_colliders_skip_the_term(oracle, device, monkeypatch, arith):
-    """Host-side early-out (parse_chain): colliders beyond the arm's reach of every node
+    """Host-side pruning (parse_chain): colliders beyond the arm's reach of every node
     (the reference's four initColliders boxes moved 1000 units away) can never pass the
-    inline sphere test, so the solver drops the term and runs the plain kernels.
+    inline sphere test, so the solver leaves them out -- with none left it drops the term
+    and runs the plain kernels; a far box beside near ones is left out alone (REFERENCE:
+    bit-exact to the oracle with all three).
     REFERENCE: bit-exact to the oracle with the colliders (its GJK runs and finds nothing)
     and to the same solver kept on the collider kernel (IKPSO_KEEP_FAR_COLLIDERS=1).
     FAST: bit-identical to a solver without colliders; a box within reach keeps the term."""
@@ -288,10 +290,17 @@ def test_far_colliders_skip_the_term(oracle, device, monkeypatch, arith):
     assert solve(edge)[0] == 0
     edge["pos"][0] = (arm, 0.0, 0.0)
     assert solve(edge)[0] == 1
+    # a far box beside near ones is left out alone
+    mixed = np.concatenate([near, far[:1]])
+    n_mixed, (angm, fitm, _) = solve(mixed)
+    assert n_mixed == 2
     if arith == "reference":
         ostate = oracle.init_generators(B * P, 0)
         oang, ofit, ores = oracle.solve_batch(wl.chain, tg, None, P, I, ostate, colliders=far, threads=8)
         assert np.array_equal(ang, oang) and np.array_equal(fit, ofit)
+        ostate = oracle.init_generators(B * P, 0)
+        oang, ofit, ores = oracle.solve_batch(wl.chain, tg, None, P, I, ostate, colliders=mixed, threads=8)
+        assert np.array_equal(angm, oang) and np.array_equal(fitm, ofit)
         monkeypatch.setenv("IKPSO_KEEP_FAR_COLLIDERS", "1")
         n_keep, (angk, fitk, _) = solve(far)
         assert n_keep == 4 and np.array_equal(angk, ang) and np.array_equal(fitk, fit)
