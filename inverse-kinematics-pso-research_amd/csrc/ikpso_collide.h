@@ -458,7 +458,7 @@ __device__ __forceinline__ bool near_collider(float nx, float ny, float nz, floa
 // within ~3.5e-4 of touching, so the two may decide differently inside that band
 // (the stated FAST tolerances: tests/test_gpu_collide.py).  The 1e-6 added to
 // |R| guards near-parallel edge pairs (a degenerate cross axis then cannot separate).
-__device__ __forceinline__ bool obb_overlap(const float a[3], const float A[9], const float ea[3], const float b[3],
+__host__ __device__ __forceinline__ bool obb_overlap(const float a[3], const float A[9], const float ea[3], const float b[3],
                                             const float B[9], const float eb[3])
 {
     float R[3][3], AR[3][3];

@@ -450,6 +450,10 @@ __device__ __forceinline__ void swarm_resident_body(const ChainConsts<Topo::J>& 
 }
 
 
+#ifndef IKPSO_COLLIDE_UNIFORM
+#define IKPSO_COLLIDE_UNIFORM 1  // the reference scene with colliders: a uniform-bounds FAST build (79.2 -> 77.2 ms)
+#endif
+
 // Waves per SIMD the resident kernel is compiled for.  The folded chain's
 // iteration is short (458 VALU instructions per wave-iteration at 7 free angles)
 // and two barriers of the swarm argmin end it: compiled for 8 waves per SIMD
@@ -554,6 +558,15 @@ inline hipError_t run_resident(const ChainHost& ch, const SwarmIO& io, int block
             hipLaunchKernelGGL((k_swarm_resident<Topo, MODE, kTermUniformBounds | kFastRev>), grid, threads, 0, stream,
                                cc, io);
             return hipGetLastError();
+        }
+        if constexpr (std::is_same_v<Topo, TopoRef7> && IKPSO_COLLIDE_UNIFORM) {
+            // the reference scene with colliders (the bench's collide leg): no runtime term tests, the clamp
+            // bounds uniform (the separating-axis builds: colliders that are rotations, angles in the unit's range)
+            if (terms == (kTermUniformBounds | kTermColliders) && ch.num_coll > 0 && ch.coll_obb && !ch.poly_trig) {
+                hipLaunchKernelGGL((k_swarm_resident<Topo, MODE, kTermUniformBounds | kTermColliders>), grid, threads, 0,
+                                   stream, cc, io);
+                return hipGetLastError();
+            }
         }
         if constexpr (std::is_same_v<Topo, TopoSerialTip<20>>) {  // BASELINE config 5's symmetric soft limits
             if (terms == (kTermUniformBounds | kTermPenalty) && ch.sym_penalty) {
