@@ -656,6 +656,9 @@ using RngFor = XorwowT<!(TERMS & kTermColliders)>;
 #ifndef IKPSO_FAST_SAT
 #define IKPSO_FAST_SAT 1
 #endif
+#ifndef IKPSO_CAND_COMPACT
+#define IKPSO_CAND_COMPACT 1
+#endif
 template <class Topo, int MODE, int TERMS>
 constexpr bool kFastSat = IKPSO_FAST_SAT && MODE == IKPSO_ARITH_FAST && (TERMS & kTermColliders) &&
                           !(TERMS & kTermMask) && !Topo::kGeneric;
@@ -731,6 +734,11 @@ struct FitnessAcc {
     // (child_frame_pinned_sc): the contact decisions of one arithmetic must not
     // depend on the kernel that makes them
     static constexpr bool kPin = (TERMS & kTermColliders) && MODE == IKPSO_ARITH_FAST;
+    // The separating-axis builds store a near node's frame as two axes and its position
+    // (9 floats instead of 16: the scratch traffic of the stored frames); the third axis
+    // is their cross product and the parent's position p - len R e_x, both recomputed
+    // in finish_for_update by every kernel alike (IKPSO_CAND_COMPACT).
+    static constexpr bool kCompactCand = IKPSO_CAND_COMPACT && kFastSat<Topo, MODE, TERMS> && kDefer;
     uint32_t near_mask;
     float* cand;
     bool hit;
@@ -862,12 +870,18 @@ struct FitnessAcc {
                                      cc.coll_lim + (k - 1) * cc.num_coll, cc.coll, cc.num_coll IKPSO_CC_STATS)) {
                 near_mask |= 1u << (k - 1);
                 float* c = cand + 16 * (k - 1);
-                c[0] = F[k].r00, c[1] = F[k].r01, c[2] = F[k].r02;
-                c[3] = F[k].r10, c[4] = F[k].r11, c[5] = F[k].r12;
-                c[6] = F[k].r20, c[7] = F[k].r21, c[8] = F[k].r22;
-                c[9] = F[k].px, c[10] = F[k].py, c[11] = F[k].pz;
-                c[12] = F[pk].px, c[13] = F[pk].py, c[14] = F[pk].pz;
-                c[15] = cc.len[k];
+                if constexpr (kCompactCand) {  // two axes and the position (finish_for_update rebuilds the rest)
+                    c[0] = F[k].r00, c[1] = F[k].r10, c[2] = F[k].r20;
+                    c[3] = F[k].r01, c[4] = F[k].r11, c[5] = F[k].r21;
+                    c[6] = F[k].px, c[7] = F[k].py, c[8] = F[k].pz;
+                } else {
+                    c[0] = F[k].r00, c[1] = F[k].r01, c[2] = F[k].r02;
+                    c[3] = F[k].r10, c[4] = F[k].r11, c[5] = F[k].r12;
+                    c[6] = F[k].r20, c[7] = F[k].r21, c[8] = F[k].r22;
+                    c[9] = F[k].px, c[10] = F[k].py, c[11] = F[k].pz;
+                    c[12] = F[pk].px, c[13] = F[pk].py, c[14] = F[pk].pz;
+                    c[15] = cc.len[k];
+                }
             }
         }
         if (node_pos) {
@@ -913,9 +927,22 @@ struct FitnessAcc {
             if (hit) f = FLT_MAX;  // (generic trees)
             uint32_t m = (f >= pbest && pbest <= FLT_MAX) ? 0u : near_mask;
             while (m != 0u) {
-                const float* c = cand + 16 * __builtin_ctz(m);
+                const int slot = __builtin_ctz(m);  // node slot + 1 = k
+                const float* c = cand + 16 * slot;
                 m &= m - 1u;
-                if constexpr (kFastSat<Topo, MODE, TERMS>) {
+                if constexpr (kCompactCand) {
+                    const int k = slot + 1;
+                    constexpr int HW = kHwTrig<Topo, MODE, TERMS>;
+                    const float a0 = c[0], a1 = c[1], a2 = c[2], b0 = c[3], b1 = c[4], b2 = c[5];
+                    const float e0 = a1 * b2 - a2 * b1, e1 = a2 * b0 - a0 * b2, e2 = a0 * b1 - a1 * b0;
+                    const float l = link_len<HW>(cc, k);
+                    const float qx = c[6] - l * a0, qy = c[7] - l * a1, qz = c[8] - l * a2;
+                    if (node_collides_obb(a0, b0, e0, a1, b1, e1, a2, b2, e2, c[6], c[7], c[8], qx, qy, qz, cc.len[k],
+                                          cc.coll, cc.coll_box, cc.num_coll)) {
+                        f = FLT_MAX;
+                        break;
+                    }
+                } else if constexpr (kFastSat<Topo, MODE, TERMS>) {
                     if (node_collides_obb(c[0], c[1], c[2], c[3], c[4], c[5], c[6], c[7], c[8], c[9], c[10], c[11],
                                           c[12], c[13], c[14], c[15], cc.coll, cc.coll_box, cc.num_coll)) {
                         f = FLT_MAX;
