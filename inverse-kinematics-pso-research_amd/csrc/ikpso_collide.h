@@ -449,6 +449,31 @@ __device__ __forceinline__ bool near_collider(float nx, float ny, float nz, floa
     return near;
 }
 
+// The same test with the first kNearUnroll colliders' centres and limits from the
+// swarm kernels' LDS copy (SwarmShared::near4, q4 = node k's 16 floats): the same
+// values and operations, so the same decisions.  One broadcast ds_read_b128 per
+// collider instead of the scalar loads of the records and limits, whose waits the
+// iteration paid on every node: collide leg 69.3 -> 66.2 ms (round 6).
+__device__ __forceinline__ bool near_collider_lds(float nx, float ny, float nz, float ex, float ey, float ez,
+                                                  const float* q4, const float* lim, const CollRec* coll, int count)
+{
+    const float mx = (nx + ex) * 0.5f, my = (ny + ey) * 0.5f, mz = (nz + ez) * 0.5f;
+    bool near = false;
+#pragma unroll
+    for (int i = 0; i < kNearUnroll; ++i)
+        if (i < count) {
+            const float4 q = *(const float4*)(q4 + 4 * i);
+            const float dx = mx - q.x, dy = my - q.y, dz = mz - q.z;
+            near = near || (dx * dx + dy * dy + dz * dz <= q.w);
+        }
+    for (int i = kNearUnroll; i < count; ++i) {
+        const CollRec& c = coll[i];
+        const float dx = mx - c.px, dy = my - c.py, dz = mz - c.pz;
+        near = near || (dx * dx + dy * dy + dz * dz <= lim[i]);
+    }
+    return near;
+}
+
 // FAST: the exact overlap test of two oriented boxes by separating axes (Gottschalk's
 // OBB test: the 3 + 3 face axes and the 9 edge-pair axes), in place of GJK.  a, b:
 // centres; A, B: axes (axis i at [3i..3i+2], unit); ea, eb: half extents.  Fixed

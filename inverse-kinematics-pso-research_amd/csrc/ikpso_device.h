@@ -742,6 +742,7 @@ struct FitnessAcc {
     uint32_t near_mask;
     float* cand;
     bool hit;
+    const float* nearc = nullptr;  // the swarm kernels' SwarmShared::near4 (near_collider_lds), else null
 
     // soft_: the soft limits -- pass the swarm kernel's LDS copy (SwarmShared::soft)
     // where there is one: a pointer that may be LDS or global is a flat pointer
@@ -866,8 +867,12 @@ struct FitnessAcc {
                                         F[k].r21, F[k].r22, F[k].px, F[k].py, F[k].pz, F[pk].px, F[pk].py, F[pk].pz,
                                         cc.len[k], cc.coll, cc.num_coll IKPSO_CC_STATS);
             } else if (cc.num_coll > 0 &&
-                       near_collider(F[k].px, F[k].py, F[k].pz, F[pk].px, F[pk].py, F[pk].pz,
-                                     cc.coll_lim + (k - 1) * cc.num_coll, cc.coll, cc.num_coll IKPSO_CC_STATS)) {
+                       (nearc ? near_collider_lds(F[k].px, F[k].py, F[k].pz, F[pk].px, F[pk].py, F[pk].pz,
+                                                  nearc + 4 * kNearUnroll * (k - 1),
+                                                  cc.coll_lim + (k - 1) * cc.num_coll, cc.coll, cc.num_coll)
+                              : near_collider(F[k].px, F[k].py, F[k].pz, F[pk].px, F[pk].py, F[pk].pz,
+                                              cc.coll_lim + (k - 1) * cc.num_coll, cc.coll,
+                                              cc.num_coll IKPSO_CC_STATS))) {
                 near_mask |= 1u << (k - 1);
                 float* c = cand + 16 * (k - 1);
                 if constexpr (kCompactCand) {  // two axes and the position (finish_for_update rebuilds the rest)

@@ -278,6 +278,8 @@ __device__ __forceinline__ void swarm_step(const ChainConsts<Topo::J>& cc, Swarm
     }
     CandBuf<Topo, TERMS> cb;
     FitnessFor<Topo, MODE, TERMS> acc(cc, sh.dh, sh.soft, cb.v);
+    if constexpr ((TERMS & kTermColliders) && SwarmShared<Topo>::kNear > 0 && !IKPSO_COLLIDE_STATS)
+        acc.nearc = sh.near4;  // (the counting builds count through near_collider)
     float* const s_v = s_pb + D * BLOCK;  // KV > 0: velocities [d][lane] (kVelLds)
     // node kk's local bests, global best, rest angles, target and LDS velocities
     auto load_node = [&](int kk, float (&pb)[A], float (&g)[A], float (&rest)[A], float (&tgt)[3], float (&vv)[A]) {

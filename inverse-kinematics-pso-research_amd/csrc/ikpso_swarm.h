@@ -49,6 +49,12 @@ struct SwarmShared {
     float dh[Topo::kDH ? 12 * J + 4 : 1];  // folded-chain constants (TopoDH)
     float soft[6 * J];           // soft joint limits [lo 3J | hi 3J] (penalty term): read every
                                  // iteration, so from LDS rather than the aux array in HBM
+    // the collider builds' inline sphere test (near_collider_lds): the first kNearUnroll
+    // colliders' centres and squared limits per node, {cx, cy, cz, lim} at
+    // [16 (k - 1) + 4 i], read by one broadcast ds_read_b128 each (compiled chains of
+    // <= 8 joints; the others read them from the aux array by scalar loads)
+    static constexpr int kNear = (!Topo::kGeneric && !Topo::kDH && J <= 8) ? 4 * kNearUnroll * J : 0;
+    alignas(16) float near4[kNear > 0 ? kNear : 4];
     uint32_t key[2][16];         // per-wave argmin, double-buffered by parity
     int32_t idx[2][16];
 };
@@ -102,6 +108,16 @@ __device__ __forceinline__ void stage_swarm_inputs(const ChainConsts<Topo::J>& c
         for (int n = threadIdx.x; n < 12 * J + 4; n += blockDim.x) sh.dh[n] = cc.aux[cc.dh_off + n];
     if (cc.use_penalty)
         for (int n = threadIdx.x; n < 6 * J; n += blockDim.x) sh.soft[n] = cc.aux[4 * J + n] * sc;
+    if constexpr ((TERMS & kTermColliders) && SwarmShared<Topo>::kNear > 0)
+        for (int n = threadIdx.x; n < kNearUnroll * J; n += blockDim.x) {
+            const int k = n / kNearUnroll, i = n % kNearUnroll;
+            if (i < cc.num_coll) {
+                sh.near4[4 * n + 0] = cc.coll[i].px;
+                sh.near4[4 * n + 1] = cc.coll[i].py;
+                sh.near4[4 * n + 2] = cc.coll[i].pz;
+                sh.near4[4 * n + 3] = cc.coll_lim[k * cc.num_coll + i];
+            }
+        }
 }
 
 // An angle of the kernel's units in radians (kTermRev: revolutions * 2 pi).
