@@ -221,15 +221,21 @@ __device__ __forceinline__ void swarm_step_tip(const ChainConsts<Topo::J>& cc, S
 // value spilled an iteration ago comes from HBM.  The velocities are read and
 // written once per iteration: two LDS instructions per dimension.  Round 5, the
 // collide leg's scene (4096 x 1024 x 500): 273 -> 222 ms, and 159 -> 102 ms with
-// the boxes out of reach (profiles/r05/variant_timings/collide_cmp.txt).
-template <class Topo, int TERMS>
+// the boxes out of reach (profiles/r05/variant_timings/collide_cmp.txt).  The
+// separating-axis builds have no call left (round 6): at most kVelLdsSat of them in
+// LDS, the rest in registers without a spill -- 66.3 -> 65.2 ms on the collide leg
+// (18 in LDS vs 9; 6 and 12 within 0.3 ms; profiles/r06/collcmp_near_variants.txt).
+// The REFERENCE collider builds keep them all in LDS (9 spilled 21 registers there).
+constexpr int kVelLdsSat = 9;
+template <class Topo, int MODE, int TERMS>
 __host__ __device__ constexpr int kVelLds()
 {
     constexpr int D = Topo::D, BLOCK = kResidentMaxThreads<D>();
     if (!(TERMS & kTermColliders) || D > 30) return 0;
     constexpr long spare = 163840L - (long)sizeof(SwarmShared<Topo>) - 256 - (long)D * BLOCK * 4;
     constexpr long k = spare / (BLOCK * 4);
-    return k <= 0 ? 0 : (k >= D ? D : (int)k);
+    constexpr int fit = k <= 0 ? 0 : (k >= D ? D : (int)k);
+    return kFastSat<Topo, MODE, TERMS> && fit > kVelLdsSat ? kVelLdsSat : fit;
 }
 
 // The collider builds' call (node_collides, out of line in FitnessAcc::finish) may
@@ -392,7 +398,7 @@ __device__ __forceinline__ void swarm_resident_body(const ChainConsts<Topo::J>& 
     // initParticlesKernel (src/kernel.cu:223-266)
     float x[D], v[D];
     init_particle<Topo, TERMS, BLOCK>(cc, sh, s_pb, tid, x, v, rng);
-    constexpr int KV = kVelLds<Topo, TERMS>();
+    constexpr int KV = kVelLds<Topo, MODE, TERMS>();
     float* const s_v = s_pb + D * BLOCK;  // (kVelLds)
 #pragma unroll
     for (int d = 0; d < KV; ++d) s_v[d * BLOCK + tid] = v[d];
@@ -474,7 +480,7 @@ __global__ void __launch_bounds__(kResidentMaxThreads<Topo::D>(), kResidentMinWa
     k_swarm_resident(const ChainConsts<Topo::J> cc, const SwarmIO io)
 {
     // local bests [d][lane], then the collider builds' LDS velocities (kVelLds)
-    constexpr int NPB = (Topo::D + kVelLds<Topo, TERMS>()) * kResidentMaxThreads<Topo::D>();
+    constexpr int NPB = (Topo::D + kVelLds<Topo, MODE, TERMS>()) * kResidentMaxThreads<Topo::D>();
     if constexpr (Topo::kGeneric) {
         // generic trees keep two arrays: hipcc 7.2 miscompiles them over one
         // LDS object (an illegal flat-to-LDS check)
